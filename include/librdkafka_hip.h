@@ -1,0 +1,156 @@
+/*
+ * librdkafka_hip.h -- C ABI of librdkafka_hip.so, the MI355X (gfx950) engine
+ * for librdkafka's per-MessageSet data-parallel work: CRC32C over MsgVersion 2
+ * record batches and LZ4F frame compression / decompression.
+ *
+ * Two layers:
+ *
+ *  1. DROP-IN symbols.  Exactly the internal librdkafka v1.3.0 functions the
+ *     MessageSet writer/reader call through the PLT, with identical
+ *     signatures, ownership and error contracts.  Preloading (or linking
+ *     ahead of librdkafka.so) interposes them; see INTEGRATION.md.
+ *
+ *  2. ENGINE batch API (rdk_hip_*).  Device-resident batches of many
+ *     toppars' record batches, processed in one launch per stage on a caller
+ *     stream.  Plain pointers and sizes only; `stream` is a hipStream_t
+ *     passed as void* (NULL = the engine's own per-thread stream).
+ *
+ * Every function that touches the GPU fails loudly (returns RDK_HIP_E_* or,
+ * for the drop-in symbols, which have no error channel, prints and aborts)
+ * when no gfx950 device / code object is available.  There is no silent CPU
+ * path; the only CPU work in the engine is frame-header bookkeeping.
+ */
+#ifndef LIBRDKAFKA_HIP_H
+#define LIBRDKAFKA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------
+ * Boundary types (opaque / mirrored).
+ * rd_slice_t is walked with the exact layout of src/rdbuf.h:63-115 (mirrored
+ * privately in csrc/rdbuf_abi.h); the broker handle is never dereferenced.
+ * ------------------------------------------------------------------------- */
+typedef struct rd_slice_s rd_slice_t;
+typedef struct rd_kafka_broker_s rd_kafka_broker_t;
+typedef int rd_kafka_resp_err_t; /* enum in rdkafka.h:258-268 */
+
+#define RDK_HIP_RESP_ERR_NO_ERROR 0
+#define RDK_HIP_RESP_ERR__BAD_MSG (-199)            /* rdkafka.h:258 */
+#define RDK_HIP_RESP_ERR__BAD_COMPRESSION (-198)    /* rdkafka.h:260 */
+#define RDK_HIP_RESP_ERR__CRIT_SYS_RESOURCE (-194)  /* rdkafka.h:268 */
+
+/* ------------------------------------------------------------------ drop-in */
+
+/* Replaces crc32c() (src/crc32c.h:32, src/crc32c.c:360-368).  `crc` is the
+ * previous result (0 to start): crc32c(crc32c(0,a),b) == crc32c(0,a||b). */
+uint32_t crc32c(uint32_t crc, const void *buf, size_t len);
+
+/* Replaces crc32c_global_init() (src/crc32c.c:378-386): idempotent; brings
+ * up the device context and uploads the CRC tables. */
+void crc32c_global_init(void);
+
+/* Replaces rd_slice_crc32c() (src/rdbuf.c:1113-1122): CRC32C of the slice's
+ * remaining segments, leaving the slice fully consumed exactly like the
+ * rd_slice_reader() loop it replaces. */
+uint32_t rd_slice_crc32c(rd_slice_t *slice);
+
+/* Replaces rd_kafka_lz4_compress() (src/rdkafka_lz4.c:329-442).  LZ4F frame
+ * with prefs {blockIndependent, comp_level}, 64 KB blocks; *outbuf is
+ * malloc()ed (caller frees with free()); slice is consumed.  comp_level >= 3
+ * (LZ4HC) is not implemented on the GPU: the call is forwarded to the next
+ * definition of the symbol (librdkafka's own) when one is loaded, otherwise
+ * __BAD_COMPRESSION is returned (the writer then sends uncompressed,
+ * rdkafka_msgset_writer.c:1175). */
+rd_kafka_resp_err_t rd_kafka_lz4_compress(rd_kafka_broker_t *rkb, int proper_hc,
+                                          int comp_level, rd_slice_t *slice,
+                                          void **outbuf, size_t *outlenp);
+
+/* Replaces rd_kafka_lz4_decompress() (src/rdkafka_lz4.c:167-317).  *outbuf
+ * is malloc()ed.  May modify inbuf only when !proper_hc.  The output buffer
+ * is sized exactly from the frame's block table, so rkb_c.zbuf_grow is never
+ * incremented (documented divergence; rkb is not dereferenced). */
+rd_kafka_resp_err_t rd_kafka_lz4_decompress(rd_kafka_broker_t *rkb, int proper_hc,
+                                            int64_t Offset, char *inbuf, size_t inlen,
+                                            void **outbuf, size_t *outlenp);
+
+/* ------------------------------------------------------------- engine API */
+#define RDK_HIP_OK 0
+#define RDK_HIP_E_NODEV (-1)      /* no usable gfx950 device / code object */
+#define RDK_HIP_E_HIP (-2)        /* HIP runtime error (launch, alloc, copy) */
+#define RDK_HIP_E_INVAL (-3)      /* bad argument */
+#define RDK_HIP_E_NOMEM (-4)
+
+/* Bind the calling thread's engine context to `device` (default: device 0 or
+ * $RDK_HIP_DEVICE).  Safe to call repeatedly. */
+int rdk_hip_init(int device);
+const char *rdk_hip_last_error(void);
+/* Engine build/feature string (arch, kernel variants). */
+const char *rdk_hip_version(void);
+
+/* CRC32C of n independent byte ranges of device memory.
+ *   d_base + d_offs[i], length d_lens[i]; init crc d_init[i] (NULL = 0);
+ *   result -> d_out[i].  Same chaining semantics as crc32c(). */
+int rdk_hip_crc32c_ranges(const void *d_base, const uint64_t *d_offs,
+                          const uint32_t *d_lens, const uint32_t *d_init,
+                          uint32_t *d_out, uint32_t n, void *stream);
+
+/* MsgVersion 2 record batches laid out at d_base + d_batch_offs[i].  The CRC
+ * range is [21, 12+Length) read from each header (big-endian Length at 8),
+ * as computed by rd_kafka_msgset_writer_calc_crc_v2
+ * (rdkafka_msgset_writer.c:1229-1246) and verified by
+ * rd_kafka_msgset_reader_v2 (rdkafka_msgset_reader.c:982-1015).
+ *   mode RDK_HIP_V2_CRC_COMPUTE : d_out[i] = crc
+ *   mode RDK_HIP_V2_CRC_FINALIZE: also store it big-endian at offset 17
+ *   mode RDK_HIP_V2_CRC_VERIFY  : d_out[i] = (crc == stored) ? 0 : 1
+ * Batches whose Length is < 9 or exceeds d_batch_caps[i]-12 get d_out = 2
+ * (VERIFY) / are skipped. */
+#define RDK_HIP_V2_CRC_COMPUTE 0
+#define RDK_HIP_V2_CRC_FINALIZE 1
+#define RDK_HIP_V2_CRC_VERIFY 2
+int rdk_hip_msgset_v2_crc(void *d_base, const uint64_t *d_batch_offs,
+                          const uint32_t *d_batch_caps, uint32_t *d_out,
+                          uint32_t n, int mode, void *stream);
+
+/* LZ4F compression of n independent inputs (rd_kafka_lz4_compress semantics
+ * per input, prefs {blockIndependent, level}).  Frame i is written to
+ * d_out + d_out_offs[i] (capacity rdk_hip_lz4f_compress_bound(len)); its
+ * size goes to d_out_lens[i].  `level` as compression.level (<3). */
+size_t rdk_hip_lz4f_compress_bound(size_t len);
+int rdk_hip_lz4f_compress(const void *d_in, const uint64_t *d_in_offs,
+                          const uint32_t *d_in_lens, void *d_out,
+                          const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                          uint32_t n, int level, void *stream);
+
+/* LZ4F decompression of n independent frames (rd_kafka_lz4_decompress
+ * semantics per frame, proper HC).  Frame i decodes into
+ * d_out + d_out_offs[i] with capacity d_out_caps[i]; d_out_lens[i] gets the
+ * decoded size and d_status[i] the rd_kafka_resp_err_t (0, __BAD_MSG,
+ * __BAD_COMPRESSION) or RDK_HIP_LZ4F_E_DSTSIZE when the capacity is short. */
+#define RDK_HIP_LZ4F_E_DSTSIZE (-1000)
+int rdk_hip_lz4f_decompress(const void *d_in, const uint64_t *d_in_offs,
+                            const uint32_t *d_in_lens, void *d_out,
+                            const uint64_t *d_out_offs, const uint32_t *d_out_caps,
+                            uint32_t *d_out_lens, int32_t *d_status, uint32_t n,
+                            void *stream);
+
+/* Deterministic synthetic workloads generated on the device (bench/tests).
+ * v2 batches: n batches of `batch_size` bytes at i*batch_size: a valid 61-byte
+ * v2 header (Magic 2, Length = batch_size-12, RecordCount) followed by
+ * splitmix64(seed) bytes; CRC field left 0. */
+int rdk_hip_gen_v2_batches(void *d_base, uint32_t n, uint32_t batch_size,
+                           uint64_t seed, void *stream);
+
+/* Host-side JSON-like record stream (DESIGN.md "Workloads"): exactly `len`
+ * bytes of `{"id":..,"user":"u.....","ts":..,"event":"..","value":..}\n`
+ * records from the LCG s = s*1103515245+12345 seeded with `seed`. */
+void rdk_hip_gen_json(uint8_t *dst, size_t len, uint32_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIBRDKAFKA_HIP_H */

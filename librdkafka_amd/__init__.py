@@ -1,0 +1,286 @@
+"""librdkafka_amd -- MI355X (gfx950) engine for librdkafka's record-batch hot path.
+
+Host-side mirror of the reference interface for this path (CRC32C over
+MsgVersion 2 record batches, LZ4F frame compression / decompression), bound
+to the C-ABI library ``librdkafka_hip.so`` built in-tree from ``csrc/``.
+
+Two layers, as in ``include/librdkafka_hip.h``:
+
+* drop-in functions with the reference's names, argument meaning and error
+  codes: :func:`crc32c`, :func:`rd_slice_crc32c`, :func:`rd_kafka_lz4_compress`,
+  :func:`rd_kafka_lz4_decompress` (host buffers in, host bytes out);
+* the device-resident batch engine (``*_batch`` functions on torch device
+  tensors) used by bench.py and the multi-partition producer/consumer paths.
+
+There is no CPU fallback: if the library or a gfx950 device is missing every
+call raises :class:`EngineError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+try:  # share torch's HIP runtime (same SONAME) when torch is present
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is always installed here
+    torch = None
+
+from . import workload  # noqa: E402,F401
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librdkafka_hip.so")
+
+RESP_ERR_NO_ERROR = 0
+RESP_ERR__BAD_MSG = -199
+RESP_ERR__BAD_COMPRESSION = -198
+RESP_ERR__CRIT_SYS_RESOURCE = -194
+LZ4F_E_DSTSIZE = -1000
+
+V2_CRC_COMPUTE, V2_CRC_FINALIZE, V2_CRC_VERIFY = 0, 1, 2
+
+# every symbol include/librdkafka_hip.h declares (checked by tests)
+EXPORTED_SYMBOLS = (
+    "crc32c", "crc32c_global_init", "rd_slice_crc32c", "rd_kafka_lz4_compress",
+    "rd_kafka_lz4_decompress", "rdk_hip_init", "rdk_hip_last_error", "rdk_hip_version",
+    "rdk_hip_crc32c_ranges", "rdk_hip_msgset_v2_crc", "rdk_hip_lz4f_compress_bound",
+    "rdk_hip_lz4f_compress", "rdk_hip_lz4f_decompress", "rdk_hip_gen_v2_batches",
+    "rdk_hip_gen_json",
+)
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def build(jobs: int = 8) -> str:
+    """Compile librdkafka_hip.so for gfx950 in-tree (hipcc)."""
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    """Load librdkafka_hip.so (raises EngineError when it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineError(f"{LIB_PATH} not built (run librdkafka_amd.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, sz, u32, i32, i64 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_int, C.c_int64
+    L.crc32c.restype = u32
+    L.crc32c.argtypes = [u32, vp, sz]
+    L.crc32c_global_init.restype = None
+    L.rd_slice_crc32c.restype = u32
+    L.rd_slice_crc32c.argtypes = [vp]
+    L.rd_kafka_lz4_compress.restype = i32
+    L.rd_kafka_lz4_compress.argtypes = [vp, i32, i32, vp, C.POINTER(vp), C.POINTER(sz)]
+    L.rd_kafka_lz4_decompress.restype = i32
+    L.rd_kafka_lz4_decompress.argtypes = [vp, i32, i64, vp, sz, C.POINTER(vp), C.POINTER(sz)]
+    L.rdk_hip_init.restype = i32
+    L.rdk_hip_init.argtypes = [i32]
+    L.rdk_hip_last_error.restype = C.c_char_p
+    L.rdk_hip_version.restype = C.c_char_p
+    L.rdk_hip_crc32c_ranges.restype = i32
+    L.rdk_hip_crc32c_ranges.argtypes = [vp, vp, vp, vp, vp, u32, vp]
+    L.rdk_hip_msgset_v2_crc.restype = i32
+    L.rdk_hip_msgset_v2_crc.argtypes = [vp, vp, vp, vp, u32, i32, vp]
+    if hasattr(L, "rdk_hip_lz4f_compress"):
+        L.rdk_hip_lz4f_compress_bound.restype = sz
+        L.rdk_hip_lz4f_compress_bound.argtypes = [sz]
+        L.rdk_hip_lz4f_compress.restype = i32
+        L.rdk_hip_lz4f_compress.argtypes = [vp, vp, vp, vp, vp, vp, u32, i32, vp]
+        L.rdk_hip_lz4f_decompress.restype = i32
+        L.rdk_hip_lz4f_decompress.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
+    L.rdk_hip_gen_v2_batches.restype = i32
+    L.rdk_hip_gen_v2_batches.argtypes = [vp, u32, u32, C.c_uint64, vp]
+    L.rdk_hip_gen_json.restype = None
+    L.rdk_hip_gen_json.argtypes = [vp, sz, u32]
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().rdk_hip_last_error().decode(errors="replace")
+        raise EngineError(f"{what} failed ({rc}): {msg}")
+
+
+def init(device: int = -1) -> None:
+    """Bind the calling thread's engine context to `device` (default 0)."""
+    _check(lib().rdk_hip_init(device), "rdk_hip_init")
+
+
+def version() -> str:
+    return lib().rdk_hip_version().decode()
+
+
+# ------------------------------------------------------------------ drop-in
+class _Segment(C.Structure):
+    pass
+
+
+_Segment._fields_ = [
+    ("tqe_next", C.POINTER(_Segment)), ("tqe_prev", C.c_void_p),
+    ("seg_p", C.c_void_p), ("seg_of", C.c_size_t), ("seg_size", C.c_size_t),
+    ("seg_absof", C.c_size_t), ("seg_free", C.c_void_p), ("seg_flags", C.c_int),
+]
+
+
+class _Slice(C.Structure):
+    _fields_ = [("buf", C.c_void_p), ("seg", C.POINTER(_Segment)), ("rof", C.c_size_t),
+                ("start", C.c_size_t), ("end", C.c_size_t)]
+
+
+class RdSlice:
+    """An rd_slice_t over a list of byte segments (rdbuf.h:63-115 layout),
+    the boundary type the writer hands to rd_slice_crc32c / lz4_compress.
+    `start`/`end` are absolute offsets into the concatenated segments."""
+
+    def __init__(self, segments, start: int = 0, end: int | None = None):
+        self._bufs = [C.create_string_buffer(bytes(s), max(1, len(s))) for s in segments]
+        n = len(segments)
+        self._segs = (_Segment * max(1, n))()
+        absof = 0
+        for i, s in enumerate(segments):
+            g = self._segs[i]
+            g.seg_p = C.addressof(self._bufs[i])
+            g.seg_of = len(s)
+            g.seg_size = len(s)
+            g.seg_absof = absof
+            absof += len(s)
+            if i + 1 < n:
+                g.tqe_next = C.pointer(self._segs[i + 1])
+        total = absof
+        end = total if end is None else end
+        self.slice = _Slice()
+        self.slice.start, self.slice.end = start, end
+        # rd_slice_init: position the reader at `start`
+        seg_i, rof = 0, start
+        while seg_i < n - 1 and rof >= len(segments[seg_i]) and len(segments[seg_i]) > 0:
+            rof -= len(segments[seg_i])
+            seg_i += 1
+        if n:
+            self.slice.seg = C.pointer(self._segs[seg_i])
+        self.slice.rof = rof
+
+    def remains(self) -> int:
+        s = self.slice
+        if not s.seg:
+            return s.end
+        return s.end - (s.seg.contents.seg_absof + s.rof)
+
+    @property
+    def ptr(self):
+        return C.byref(self.slice)
+
+
+def crc32c(crc: int, data: bytes) -> int:
+    """crc32c() (src/crc32c.c:360) on the GPU."""
+    b = C.create_string_buffer(bytes(data), max(1, len(data)))
+    return lib().crc32c(crc & 0xFFFFFFFF, b, len(data))
+
+
+def rd_slice_crc32c(slice_or_segments) -> int:
+    """rd_slice_crc32c() (src/rdbuf.c:1113) on the GPU; consumes the slice."""
+    s = slice_or_segments if isinstance(slice_or_segments, RdSlice) else RdSlice(slice_or_segments)
+    return lib().rd_slice_crc32c(s.ptr)
+
+
+def rd_kafka_lz4_compress(proper_hc: int, comp_level: int, slice_or_segments) -> tuple[int, bytes]:
+    """rd_kafka_lz4_compress() (src/rdkafka_lz4.c:329): (err, frame)."""
+    s = slice_or_segments if isinstance(slice_or_segments, RdSlice) else RdSlice(
+        [slice_or_segments] if isinstance(slice_or_segments, (bytes, bytearray)) else slice_or_segments)
+    out = C.c_void_p()
+    n = C.c_size_t()
+    err = lib().rd_kafka_lz4_compress(None, proper_hc, comp_level, s.ptr, C.byref(out), C.byref(n))
+    if err:
+        return err, b""
+    res = C.string_at(out, n.value)
+    _libc().free(out)
+    return 0, res
+
+
+def rd_kafka_lz4_decompress(proper_hc: int, offset: int, frame) -> tuple[int, bytes]:
+    """rd_kafka_lz4_decompress() (src/rdkafka_lz4.c:167): (err, payload).
+    `frame` may be a bytearray, which is patched in place when !proper_hc."""
+    buf = C.create_string_buffer(bytes(frame), max(1, len(frame)))
+    out = C.c_void_p()
+    n = C.c_size_t()
+    err = lib().rd_kafka_lz4_decompress(None, proper_hc, offset, buf, len(frame),
+                                        C.byref(out), C.byref(n))
+    if isinstance(frame, bytearray):
+        frame[:] = buf.raw[:len(frame)]
+    if err:
+        return err, b""
+    res = C.string_at(out, n.value) if n.value else b""
+    _libc().free(out)
+    return 0, res
+
+
+_libc_h = None
+
+
+def _libc():
+    global _libc_h
+    if _libc_h is None:
+        _libc_h = C.CDLL(None)
+        _libc_h.free.argtypes = [C.c_void_p]
+    return _libc_h
+
+
+# ------------------------------------------------------- device batch engine
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    return C.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+
+
+def crc32c_ranges(base, offs, lens, out, init=None, stream=None) -> None:
+    """CRC32C of device ranges base[offs[i]:offs[i]+lens[i]] -> out[i] (uint32)."""
+    _check(lib().rdk_hip_crc32c_ranges(_ptr(base), _ptr(offs), _ptr(lens), _ptr(init), _ptr(out),
+                                       int(offs.numel()), _stream(stream)), "crc32c_ranges")
+
+
+def msgset_v2_crc(base, batch_offs, batch_caps, out, mode=V2_CRC_COMPUTE, stream=None) -> None:
+    """CRC32C compute / finalize / verify of MsgVersion 2 batches on device."""
+    _check(lib().rdk_hip_msgset_v2_crc(_ptr(base), _ptr(batch_offs), _ptr(batch_caps), _ptr(out),
+                                       int(batch_offs.numel()), mode, _stream(stream)),
+           "msgset_v2_crc")
+
+
+def lz4f_compress_bound(n: int) -> int:
+    return int(lib().rdk_hip_lz4f_compress_bound(n))
+
+
+def lz4f_compress_batch(src, in_offs, in_lens, dst, out_offs, out_lens, level=0, stream=None):
+    _check(lib().rdk_hip_lz4f_compress(_ptr(src), _ptr(in_offs), _ptr(in_lens), _ptr(dst),
+                                       _ptr(out_offs), _ptr(out_lens), int(in_offs.numel()),
+                                       level, _stream(stream)), "lz4f_compress")
+
+
+def lz4f_decompress_batch(src, in_offs, in_lens, dst, out_offs, out_caps, out_lens, status,
+                          stream=None):
+    _check(lib().rdk_hip_lz4f_decompress(_ptr(src), _ptr(in_offs), _ptr(in_lens), _ptr(dst),
+                                         _ptr(out_offs), _ptr(out_caps), _ptr(out_lens),
+                                         _ptr(status), int(in_offs.numel()), _stream(stream)),
+           "lz4f_decompress")
+
+
+def gen_v2_batches(base, n: int, batch_size: int, seed: int = 0x5EED, stream=None) -> None:
+    _check(lib().rdk_hip_gen_v2_batches(_ptr(base), n, batch_size, seed, _stream(stream)),
+           "gen_v2_batches")
+
+
+def gen_json(n: int, seed: int = 42) -> bytes:
+    """Native JSON-like record generator (same bytes as workload.gen_json)."""
+    b = C.create_string_buffer(max(1, n))
+    lib().rdk_hip_gen_json(b, n, seed)
+    return b.raw[:n]

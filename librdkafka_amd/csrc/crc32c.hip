@@ -1,0 +1,358 @@
+// crc32c.hip -- CRC32C kernels for gfx950 (MI355X).
+//
+// Replaces crc32c() (src/crc32c.c:360) / rd_slice_crc32c() (src/rdbuf.c:1113)
+// as called by the MessageSet writer (rdkafka_msgset_writer.c:1229-1246) and
+// reader (rdkafka_msgset_reader.c:982-1015).
+//
+// Design (DESIGN.md "CRC32C"):
+//   * one wavefront per byte range (a record batch), persistent grid;
+//   * lane l of iteration k owns the 16-byte vector at V + 1024k + 16l, so
+//     every global_load_dwordx4 of the wave reads 1 KiB contiguous (coalesced);
+//   * a lane folds its vectors into a raw CRC register with 16 slicing-table
+//     lookups + a 4-lookup "advance 1024 bytes" operator (tables in LDS);
+//   * the 64 lane registers are merged by a 6-level xor-shuffle tree whose
+//     level m applies the "advance 16*2^m bytes" operator -- the GF(2)
+//     combine of crc32c.c:144-231 generalised from 3 streams to 64 lanes;
+//   * unaligned starts are zero-masked (leading zeros do not change a raw
+//     CRC), the caller's running crc is injected by xor into the first four
+//     message bytes, and the <16-byte tail is folded in by the last lane.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "crc32c_tables.h"
+
+namespace rdk {
+
+constexpr int kCrcBlock = 512;       // threads per workgroup (8 waves)
+constexpr int kCrcSmall = 64;        // ranges shorter than this: serial lane
+constexpr uint32_t kCrcChunk = 65536; // split of long single ranges
+
+// LDS-qualified pointer: keeps table lookups as ds_read_b32 with an immediate
+// table offset instead of generic (flat) address arithmetic.
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+
+__device__ __forceinline__ uint32_t L8(const lds_u32 *L, int table, uint32_t byte) {
+  return L[(table << 8) + byte];
+}
+
+// raw CRC register advanced by 4 zero bytes... n bytes via a 4x256 operator
+__device__ __forceinline__ uint32_t shift_op(const lds_u32 *L, int base, uint32_t x) {
+  return L8(L, base, x & 0xffu) ^ L8(L, base + 1, (x >> 8) & 0xffu) ^
+         L8(L, base + 2, (x >> 16) & 0xffu) ^ L8(L, base + 3, x >> 24);
+}
+
+// advance 16 bytes: state byte j is followed by 15-j bytes -> T[15-j]
+__device__ __forceinline__ uint32_t shift16(const lds_u32 *L, uint32_t x) {
+  return L8(L, 15, x & 0xffu) ^ L8(L, 14, (x >> 8) & 0xffu) ^
+         L8(L, 13, (x >> 16) & 0xffu) ^ L8(L, 12, x >> 24);
+}
+
+// raw CRC (zero register) of one 16-byte vector, byte i -> T[15-i]
+__device__ __forceinline__ uint32_t raw16(const lds_u32 *L, uint4 w) {
+  uint32_t a = L8(L, 15, w.x & 0xffu) ^ L8(L, 14, (w.x >> 8) & 0xffu) ^
+               L8(L, 13, (w.x >> 16) & 0xffu) ^ L8(L, 12, w.x >> 24);
+  uint32_t b = L8(L, 11, w.y & 0xffu) ^ L8(L, 10, (w.y >> 8) & 0xffu) ^
+               L8(L, 9, (w.y >> 16) & 0xffu) ^ L8(L, 8, w.y >> 24);
+  uint32_t c = L8(L, 7, w.z & 0xffu) ^ L8(L, 6, (w.z >> 8) & 0xffu) ^
+               L8(L, 5, (w.z >> 16) & 0xffu) ^ L8(L, 4, w.z >> 24);
+  uint32_t d = L8(L, 3, w.w & 0xffu) ^ L8(L, 2, (w.w >> 8) & 0xffu) ^
+               L8(L, 1, (w.w >> 16) & 0xffu) ^ L8(L, 0, w.w >> 24);
+  return (a ^ b) ^ (c ^ d);
+}
+
+// Zero the bytes of dword [d, d+4) that precede `s`, and xor the 4-byte
+// injected register `ninit` (placed at byte address s) into it.
+__device__ __forceinline__ uint32_t head_fix(uint32_t v, uintptr_t d, uintptr_t s, uint32_t ninit) {
+  if (d + 4 <= s) v = 0;
+  else if (d < s) v &= 0xffffffffu << (8u * uint32_t(s - d));
+  long rel = long(s) - long(d);
+  if (rel >= 0 && rel < 4) v ^= ninit << (8u * uint32_t(rel));
+  else if (rel < 0 && rel > -4) v ^= ninit >> (8u * uint32_t(-rel));
+  return v;
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gbl_u32x4;
+__device__ __forceinline__ uint4 ldg16(uintptr_t a) {
+  // streamed once: non-temporal hint keeps it from evicting L2-resident tables
+  const u32x4 v = __builtin_nontemporal_load((gbl_u32x4 *)a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// CRC32C of [s, e) by one wavefront.  `inject`: the range starts a message
+// whose previous crc is `init` (crc32c() chaining); `final`: return the
+// inverted crc32c() value, else the raw register (for later combining).
+// The result is valid in every lane.
+__device__ __attribute__((always_inline)) uint32_t wave_crc(uintptr_t s, uintptr_t e,
+                                                           uint32_t init, bool inject,
+                                                           bool final, const lds_u32 *L,
+                                                           int lane) {
+  const size_t len = e - s;
+  uint32_t x;
+  if (len < size_t(kCrcSmall)) {
+    uint32_t c = inject ? ~init : 0u;
+    if (lane == 0) {
+      typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
+      gbl_u8 *p = (gbl_u8 *)s;
+      for (size_t i = 0; i < len; ++i) c = L8(L, 0, (c ^ p[i]) & 0xffu) ^ (c >> 8);
+    }
+    x = __builtin_amdgcn_readfirstlane(c);
+    return final ? ~x : x;
+  }
+  const uintptr_t A = s & ~uintptr_t(15), B = e & ~uintptr_t(15);
+  const uint32_t nb = uint32_t((B - A) >> 4);
+  const uint32_t K = (nb + 63u) >> 6;
+  const uintptr_t V = B - uintptr_t(K) * 1024u;
+  const uint32_t ninit = inject ? ~init : 0u;
+  const int sh1024 = crc_shift_table(6);
+
+  uintptr_t blk = V + uintptr_t(lane) * 16u;
+  uint4 nxt = make_uint4(0, 0, 0, 0);
+  if (blk >= A) nxt = ldg16(blk);
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < K; ++k) {
+    uint4 w = nxt;
+    const uintptr_t cb = blk;
+    blk += 1024u;
+    if (k + 1 < K) nxt = ldg16(blk);  // software prefetch of the next 1 KiB
+    if (cb < A + 32u) {
+      w.x = head_fix(w.x, cb, s, ninit);
+      w.y = head_fix(w.y, cb + 4, s, ninit);
+      w.z = head_fix(w.z, cb + 8, s, ninit);
+      w.w = head_fix(w.w, cb + 12, s, ninit);
+    }
+    if (k) r = shift_op(L, sh1024, r);
+    r ^= raw16(L, w);
+  }
+  // 64-lane merge tree: lane l (bit m set) absorbs lane l-2^m, 16*2^m earlier
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    uint32_t y = (m == 0) ? shift16(L, r) : shift_op(L, crc_shift_table(m), r);
+    y = __shfl_xor(y, 1 << m);
+    if (lane & (1 << m)) r ^= y;
+  }
+  // lane 63 now holds the register for [A, B); fold the tail [B, e)
+  const uint32_t t = uint32_t(e - B);
+  if (lane == 63 && t) {
+    const uint4 tw = ldg16(B);
+    uint32_t y = (t < 4) ? (r >> (8u * t)) : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+      if (j < t) y ^= L8(L, int(t - 1 - j), (r >> (8 * j)) & 0xffu);
+    const uint32_t tv[4] = {tw.x, tw.y, tw.z, tw.w};
+#pragma unroll
+    for (uint32_t i = 0; i < 15; ++i)
+      if (i < t) y ^= L8(L, int(t - 1 - i), (tv[i >> 2] >> (8 * (i & 3))) & 0xffu);
+    r = y;
+  }
+  x = __builtin_amdgcn_readlane(r, 63);
+  return final ? ~x : x;
+}
+
+__device__ __forceinline__ void load_tables(uint32_t *L, const uint32_t *g) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(g);
+  uint4 *dst = reinterpret_cast<uint4 *>(L);
+  for (int i = threadIdx.x; i < kCrcTableWords / 4; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t be32_at(const uint8_t *p) {
+  return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
+}
+
+// ---- independent ranges ---------------------------------------------------
+__global__ __launch_bounds__(kCrcBlock) void crc32c_ranges_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint32_t *__restrict__ lens, const uint32_t *__restrict__ init,
+    uint32_t *__restrict__ out, uint32_t n, const uint32_t *__restrict__ gtab) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[kCrcTableWords];
+  load_tables(L, gtab);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t wave = blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const lds_u32 *Lt = (const lds_u32 *)L;
+  for (uint32_t i = wave; i < n; i += gridDim.x * wpb) {
+    const uintptr_t s = reinterpret_cast<uintptr_t>(base) + offs[i];
+    const uint32_t c0 = init ? init[i] : 0u;
+    const uint32_t crc = wave_crc(s, s + lens[i], c0, true, true, Lt, lane);
+    if (lane == 0) out[i] = crc;
+  }
+}
+
+// ---- one long range split into kCrcChunk chunks (raw registers) ------------
+__global__ __launch_bounds__(kCrcBlock) void crc32c_chunks_kernel(
+    const uint8_t *__restrict__ p, uint64_t len, uint32_t init, uint32_t *__restrict__ raw,
+    uint32_t nchunks, const uint32_t *__restrict__ gtab) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[kCrcTableWords];
+  load_tables(L, gtab);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t wave = blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const lds_u32 *Lt = (const lds_u32 *)L;
+  for (uint32_t i = wave; i < nchunks; i += gridDim.x * wpb) {
+    const uint64_t o = uint64_t(i) * kCrcChunk;
+    const uint64_t l = (len - o < kCrcChunk) ? len - o : kCrcChunk;
+    const uintptr_t s = reinterpret_cast<uintptr_t>(p) + o;
+    const uint32_t r = wave_crc(s, s + l, init, i == 0, false, Lt, lane);
+    if (lane == 0) raw[i] = r;
+  }
+}
+
+// multiply in GF(2)[x]/P, reflected (bit 31 = x^0)
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (int i = 0; i < 32; ++i) {
+    if (a & m) p ^= b;
+    m >>= 1;
+    b = (b & 1u) ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+
+// register advanced by `nbytes` zero bytes
+__device__ uint32_t shift_bytes(uint32_t x, uint64_t nbytes, const uint32_t *x2n) {
+  uint32_t p = 1u << 31;
+  int k = 3;
+  for (uint64_t n = nbytes; n; n >>= 1, ++k)
+    if (n & 1u) p = multmodp(x2n[k], p);
+  return multmodp(p, x);
+}
+
+__global__ void crc32c_combine_kernel(const uint32_t *__restrict__ raw, uint32_t nchunks,
+                                      uint64_t len, uint32_t *__restrict__ out,
+                                      const uint32_t *__restrict__ x2n) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t x = raw[0];
+  for (uint32_t i = 1; i < nchunks; ++i) {
+    const uint64_t o = uint64_t(i) * kCrcChunk;
+    const uint64_t l = (len - o < kCrcChunk) ? len - o : kCrcChunk;
+    x = shift_bytes(x, l, x2n) ^ raw[i];
+  }
+  *out = ~x;
+}
+
+// ---- MsgVersion 2 record batches ------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kCrcBlock) void crc32c_msgset_v2_kernel(
+    uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint32_t *__restrict__ caps, uint32_t *__restrict__ out, uint32_t n,
+    const uint32_t *__restrict__ gtab) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[kCrcTableWords];
+  load_tables(L, gtab);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t wave = blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const lds_u32 *Lt = (const lds_u32 *)L;
+  for (uint32_t i = wave; i < n; i += gridDim.x * wpb) {
+    uint8_t *hdr = base + offs[i];
+    const uint32_t length = be32_at(hdr + 8);  // RD_KAFKAP_MSGSET_V2_OF_Length
+    const uint32_t cap = caps[i];
+    if (length < 9u || uint64_t(length) + 12u > cap) {  // crc_len = Length-4-1-4
+      if (lane == 0) out[i] = (MODE == RDK_HIP_V2_CRC_VERIFY) ? 2u : 0u;
+      continue;
+    }
+    const uintptr_t s = reinterpret_cast<uintptr_t>(hdr) + 21u;
+    const uintptr_t e = reinterpret_cast<uintptr_t>(hdr) + 12u + length;
+    const uint32_t crc = wave_crc(s, e, 0u, true, true, Lt, lane);
+    if (lane == 0) {
+      if (MODE == RDK_HIP_V2_CRC_VERIFY) {
+        out[i] = (be32_at(hdr + 17) == crc) ? 0u : 1u;
+      } else {
+        out[i] = crc;
+        if (MODE == RDK_HIP_V2_CRC_FINALIZE) {  // rd_kafka_buf_update_i32 (BE)
+          hdr[17] = uint8_t(crc >> 24);
+          hdr[18] = uint8_t(crc >> 16);
+          hdr[19] = uint8_t(crc >> 8);
+          hdr[20] = uint8_t(crc);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace rdk
+
+// ============================================================ host launchers
+namespace rdk {
+
+static unsigned crc_grid(uint32_t nwork) {
+  const uint32_t wpb = kCrcBlock / kWave;
+  uint32_t blocks = (nwork + wpb - 1) / wpb;
+  // 40 KiB LDS per workgroup -> 4 resident per CU; 256 CUs
+  if (blocks > 1024u) blocks = 1024u;
+  return blocks ? blocks : 1u;
+}
+
+// CRC32C of one device buffer (any length) -> *d_result (device).  Used by the
+// drop-in crc32c()/rd_slice_crc32c() after the host gather + H2D copy.
+int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
+                      uint32_t *d_scratch /* >= nchunks+1 words */, hipStream_t s) {
+  const uint32_t nchunks = len ? uint32_t((len + kCrcChunk - 1) / kCrcChunk) : 1u;
+  const uint32_t *tab = crc_tables_dev(c->device);
+  if (len == 0) {
+    // crc32c(crc, buf, 0) == crc: inversions cancel (crc32c.c:102,133)
+    RDK_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_scratch + nchunks), init, 1, s));
+    return 0;
+  }
+  hipLaunchKernelGGL(crc32c_chunks_kernel, dim3(crc_grid(nchunks)), dim3(kCrcBlock), 0, s, d_buf,
+                     len, init, d_scratch, nchunks, tab);
+  hipLaunchKernelGGL(crc32c_combine_kernel, dim3(1), dim3(64), 0, s, d_scratch, nchunks, len,
+                     d_scratch + nchunks, crc_x2n_dev(c->device));
+  RDK_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+uint32_t crc_scratch_words(uint64_t len) {
+  return (len ? uint32_t((len + kCrcChunk - 1) / kCrcChunk) : 1u) + 1u;
+}
+
+}  // namespace rdk
+
+using namespace rdk;
+
+RDK_API int rdk_hip_crc32c_ranges(const void *d_base, const uint64_t *d_offs,
+                                  const uint32_t *d_lens, const uint32_t *d_init,
+                                  uint32_t *d_out, uint32_t n, void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_base || !d_offs || !d_lens || !d_out) return set_error(RDK_HIP_E_INVAL, "null pointer");
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  hipLaunchKernelGGL(crc32c_ranges_kernel, dim3(crc_grid(n)), dim3(kCrcBlock), 0, s,
+                     static_cast<const uint8_t *>(d_base), d_offs, d_lens, d_init, d_out, n,
+                     crc_tables_dev(c->device));
+  RDK_HIP_CHECK(hipGetLastError());
+  return RDK_HIP_OK;
+}
+
+RDK_API int rdk_hip_msgset_v2_crc(void *d_base, const uint64_t *d_batch_offs,
+                                  const uint32_t *d_batch_caps, uint32_t *d_out, uint32_t n,
+                                  int mode, void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_base || !d_batch_offs || !d_batch_caps || !d_out)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  uint8_t *b = static_cast<uint8_t *>(d_base);
+  const uint32_t *tab = crc_tables_dev(c->device);
+  const dim3 g(crc_grid(n)), blk(kCrcBlock);
+  switch (mode) {
+    case RDK_HIP_V2_CRC_COMPUTE:
+      hipLaunchKernelGGL(crc32c_msgset_v2_kernel<RDK_HIP_V2_CRC_COMPUTE>, g, blk, 0, s, b,
+                         d_batch_offs, d_batch_caps, d_out, n, tab);
+      break;
+    case RDK_HIP_V2_CRC_FINALIZE:
+      hipLaunchKernelGGL(crc32c_msgset_v2_kernel<RDK_HIP_V2_CRC_FINALIZE>, g, blk, 0, s, b,
+                         d_batch_offs, d_batch_caps, d_out, n, tab);
+      break;
+    case RDK_HIP_V2_CRC_VERIFY:
+      hipLaunchKernelGGL(crc32c_msgset_v2_kernel<RDK_HIP_V2_CRC_VERIFY>, g, blk, 0, s, b,
+                         d_batch_offs, d_batch_caps, d_out, n, tab);
+      break;
+    default:
+      return set_error(RDK_HIP_E_INVAL, "bad mode %d", mode);
+  }
+  RDK_HIP_CHECK(hipGetLastError());
+  return RDK_HIP_OK;
+}

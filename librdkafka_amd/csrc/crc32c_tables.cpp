@@ -1,0 +1,82 @@
+// crc32c_tables.cpp -- see crc32c_tables.h.
+#include "crc32c_tables.h"
+
+#include <cstring>
+
+namespace rdk {
+
+uint32_t crc_gf2_times(const uint32_t mat[32], uint32_t vec) {
+  uint32_t s = 0;
+  for (int i = 0; vec; ++i, vec >>= 1)
+    if (vec & 1u) s ^= mat[i];
+  return s;
+}
+
+static void gf2_compose(uint32_t dst[32], const uint32_t a[32], const uint32_t b[32]) {
+  // dst = a o b (apply b, then a)
+  uint32_t r[32];
+  for (int i = 0; i < 32; ++i) r[i] = crc_gf2_times(a, b[i]);
+  std::memcpy(dst, r, sizeof r);
+}
+
+// Operator appending `nbytes` zero bytes to a raw (un-inverted) CRC register.
+// Column i = image of register bit i.  One zero BIT maps bit 0 -> poly and
+// bit i -> bit i-1 (reflected shift), as in crc32c_zeros_op (crc32c.c:173).
+void crc_zeros_operator(uint32_t op[32], size_t nbytes) {
+  uint32_t p[32];
+  p[0] = kCrcPoly;
+  for (int i = 1; i < 32; ++i) p[i] = 1u << (i - 1);
+  for (int k = 0; k < 3; ++k) gf2_compose(p, p, p);  // 1 bit -> 8 bits
+  for (int i = 0; i < 32; ++i) op[i] = 1u << i;        // identity
+  while (nbytes) {
+    if (nbytes & 1u) gf2_compose(op, p, op);
+    nbytes >>= 1;
+    if (nbytes) gf2_compose(p, p, p);
+  }
+}
+
+void crc_build_tables(uint32_t *out) {
+  // byte-wise table, then slicing extension (crc32c.c:69-92 generalised to 16)
+  uint32_t *T = out;
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t r = b;
+    for (int i = 0; i < 8; ++i) r = (r >> 1) ^ ((r & 1u) ? kCrcPoly : 0u);
+    T[b] = r;
+  }
+  for (int k = 1; k < kCrcSliceTables; ++k)
+    for (uint32_t b = 0; b < 256; ++b) {
+      uint32_t r = T[(k - 1) * 256 + b];
+      T[k * 256 + b] = T[r & 0xffu] ^ (r >> 8);
+    }
+  // shift operators for 32..1024 bytes, split per state byte
+  for (int level = 1; level <= 6; ++level) {
+    uint32_t op[32];
+    crc_zeros_operator(op, size_t(16) << level);
+    uint32_t *S = out + crc_shift_table(level) * 256;
+    for (int j = 0; j < 4; ++j)
+      for (uint32_t b = 0; b < 256; ++b) S[j * 256 + b] = crc_gf2_times(op, b << (8 * j));
+  }
+}
+
+// x2n[k] = x^(2^k) mod P in reflected form (bit 31 = x^0), for the
+// multiply-mod-P shift used when combining ranges of arbitrary length.
+static uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1u) ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+
+void crc_build_x2n(uint32_t *out) {
+  uint32_t p = 1u << 30;  // x^1
+  out[0] = p;
+  for (int k = 1; k < 64; ++k) out[k] = p = multmodp(p, p);
+}
+
+}  // namespace rdk

@@ -1,0 +1,170 @@
+// engine.cpp -- device/context management for librdkafka_hip.
+//
+// One context per calling thread (librdkafka calls the drop-in symbols from
+// every broker thread concurrently, rdkafka_broker.c:5082): own HIP stream,
+// own pinned staging ring and device scratch, so broker threads never
+// serialise on a shared lock.  CRC tables are uploaded once per device.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "common.h"
+#include "crc32c_tables.h"
+
+namespace rdk {
+
+static thread_local char tl_err[512];
+static thread_local Ctx *tl_ctx = nullptr;
+
+int set_error(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(tl_err, sizeof tl_err, fmt, ap);
+  va_end(ap);
+  if (getenv("RDK_HIP_DEBUG")) fprintf(stderr, "librdkafka_hip: %s\n", tl_err);
+  return code;
+}
+
+const char *last_error() { return tl_err; }
+
+[[noreturn]] void fatal(const char *what) {
+  fprintf(stderr, "librdkafka_hip: FATAL: %s: %s\n", what, tl_err[0] ? tl_err : "(no detail)");
+  fflush(stderr);
+  abort();
+}
+
+namespace {
+constexpr int kMaxDev = 64;
+std::mutex g_mu;
+uint32_t *g_tables[kMaxDev];
+uint32_t *g_x2n[kMaxDev];
+
+int default_device() {
+  const char *e = getenv("RDK_HIP_DEVICE");
+  return e ? atoi(e) : 0;
+}
+
+int upload_tables(int dev) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_tables[dev]) return 0;
+  static uint32_t host_tab[kCrcTableWords];
+  static uint32_t host_x2n[64];
+  crc_build_tables(host_tab);
+  crc_build_x2n(host_x2n);
+  uint32_t *d = nullptr, *x = nullptr;
+  RDK_HIP_CHECK(hipMalloc(&d, sizeof host_tab));
+  RDK_HIP_CHECK(hipMalloc(&x, sizeof host_x2n));
+  RDK_HIP_CHECK(hipMemcpy(d, host_tab, sizeof host_tab, hipMemcpyHostToDevice));
+  RDK_HIP_CHECK(hipMemcpy(x, host_x2n, sizeof host_x2n, hipMemcpyHostToDevice));
+  g_tables[dev] = d;
+  g_x2n[dev] = x;
+  return 0;
+}
+
+int bind(int dev) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return set_error(RDK_HIP_E_NODEV, "no HIP device visible");
+  if (dev < 0 || dev >= ndev || dev >= kMaxDev)
+    return set_error(RDK_HIP_E_INVAL, "device %d out of range (%d visible)", dev, ndev);
+  hipDeviceProp_t prop;
+  RDK_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_error(RDK_HIP_E_NODEV, "device %d is %s, engine is built for gfx950 only", dev,
+                     prop.gcnArchName);
+  RDK_HIP_CHECK(hipSetDevice(dev));
+  int rc = upload_tables(dev);
+  if (rc) return rc;
+  if (!tl_ctx) tl_ctx = new Ctx();
+  if (tl_ctx->device != dev) {
+    if (tl_ctx->stream) (void)hipStreamDestroy(tl_ctx->stream);
+    tl_ctx->stream = nullptr;
+    RDK_HIP_CHECK(hipStreamCreateWithFlags(&tl_ctx->stream, hipStreamNonBlocking));
+    tl_ctx->device = dev;
+    // device scratch belongs to the old device: drop it
+    for (int i = 0; i < 2; ++i) {
+      if (tl_ctx->d_stage[i]) (void)hipFree(tl_ctx->d_stage[i]);
+      tl_ctx->d_stage[i] = nullptr;
+      tl_ctx->d_cap[i] = 0;
+    }
+    if (tl_ctx->d_desc) (void)hipFree(tl_ctx->d_desc);
+    tl_ctx->d_desc = nullptr;
+    tl_ctx->d_desc_cap = 0;
+  }
+  return 0;
+}
+}  // namespace
+
+Ctx *ctx() {
+  if (tl_ctx && tl_ctx->device >= 0) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == tl_ctx->device) return tl_ctx;
+    (void)hipSetDevice(tl_ctx->device);
+    return tl_ctx;
+  }
+  if (bind(default_device())) return nullptr;
+  return tl_ctx;
+}
+
+static size_t grow(size_t have, size_t want) {
+  size_t n = have ? have : (size_t(1) << 20);
+  while (n < want) n *= 2;
+  return n;
+}
+
+int ensure_host(Ctx *c, size_t bytes) {
+  if (c->h_cap >= bytes) return 0;
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  c->h_stage = nullptr;
+  size_t n = grow(c->h_cap, bytes);
+  RDK_HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&c->h_stage), n, hipHostMallocDefault));
+  c->h_cap = n;
+  return 0;
+}
+
+int ensure_dev(Ctx *c, int which, size_t bytes) {
+  if (c->d_cap[which] >= bytes) return 0;
+  if (c->d_stage[which]) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->d_stage[which]);
+  }
+  c->d_stage[which] = nullptr;
+  size_t n = grow(c->d_cap[which], bytes);
+  RDK_HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&c->d_stage[which]), n));
+  c->d_cap[which] = n;
+  return 0;
+}
+
+int ensure_desc(Ctx *c, size_t bytes) {
+  if (c->d_desc_cap >= bytes) return 0;
+  if (c->d_desc) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->d_desc);
+    (void)hipHostFree(c->h_desc);
+  }
+  size_t n = grow(c->d_desc_cap, bytes);
+  RDK_HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&c->d_desc), n));
+  RDK_HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&c->h_desc), n, hipHostMallocDefault));
+  c->d_desc_cap = n;
+  return 0;
+}
+
+const uint32_t *crc_tables_dev(int device) { return g_tables[device]; }
+const uint32_t *crc_x2n_dev(int device) { return g_x2n[device]; }
+
+}  // namespace rdk
+
+RDK_API int rdk_hip_init(int device) {
+  if (device < 0) device = rdk::default_device();
+  return rdk::bind(device);
+}
+
+RDK_API const char *rdk_hip_last_error(void) { return rdk::last_error(); }
+
+RDK_API const char *rdk_hip_version(void) {
+  return "librdkafka_hip 0.1 gfx950 crc32c:wave-slice16-lds lz4c:wave-exact lz4d:wave-serial";
+}

@@ -1,0 +1,124 @@
+// shim.cpp -- the drop-in symbols (see include/librdkafka_hip.h).
+//
+// Each call gathers its input (an rd_slice_t segment list or a contiguous
+// buffer) into the calling thread's pinned staging buffer, copies it to the
+// device, runs the gfx950 kernels on the thread's own stream and copies the
+// result back into malloc() memory owned by the caller -- the ownership
+// contract of rdkafka_lz4.c (rd_free == free, rd.h:104-119).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+
+#include "common.h"
+#include "lz4_engine.h"
+#include "rdbuf_abi.h"
+
+namespace rdk {
+int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
+                      uint32_t *d_scratch, hipStream_t s);
+uint32_t crc_scratch_words(uint64_t len);
+
+// CRC32C of `len` bytes already gathered in c->h_stage.
+static int crc_staged(Ctx *c, size_t len, uint32_t init, uint32_t *out) {
+  const uint32_t words = crc_scratch_words(len);
+  int rc;
+  if ((rc = ensure_dev(c, 0, len + 64)) || (rc = ensure_desc(c, size_t(words) * 4))) return rc;
+  if (len) RDK_HIP_CHECK(hipMemcpyAsync(c->d_stage[0], c->h_stage, len, hipMemcpyHostToDevice, c->stream));
+  if ((rc = crc_device_buffer(c, c->d_stage[0], len, init,
+                              reinterpret_cast<uint32_t *>(c->d_desc), c->stream)))
+    return rc;
+  RDK_HIP_CHECK(hipMemcpyAsync(c->h_desc, c->d_desc + size_t(words - 1) * 4, 4,
+                               hipMemcpyDeviceToHost, c->stream));
+  RDK_HIP_CHECK(hipStreamSynchronize(c->stream));
+  std::memcpy(out, c->h_desc, 4);
+  return 0;
+}
+
+static Ctx *ctx_or_die(const char *who) {
+  Ctx *c = ctx();
+  if (!c) fatal(who);
+  return c;
+}
+
+}  // namespace rdk
+
+using namespace rdk;
+
+RDK_API void crc32c_global_init(void) { (void)ctx_or_die("crc32c_global_init"); }
+
+RDK_API uint32_t crc32c(uint32_t crc, const void *buf, size_t len) {
+  Ctx *c = ctx_or_die("crc32c");
+  if (len == 0) return crc;  // pre/post inversions cancel (crc32c.c:102,133)
+  if (ensure_host(c, len)) fatal("crc32c: pinned staging");
+  std::memcpy(c->h_stage, buf, len);
+  uint32_t out = 0;
+  if (crc_staged(c, len, crc, &out)) fatal("crc32c");
+  return out;
+}
+
+RDK_API uint32_t rd_slice_crc32c(rd_slice_t *slice) {
+  Ctx *c = ctx_or_die("rd_slice_crc32c");
+  const size_t total = slice_remains(slice);
+  if (ensure_host(c, total ? total : 1)) fatal("rd_slice_crc32c: pinned staging");
+  // iovec gather (rdbuf.c:1118-1119 loop) into the pinned staging buffer;
+  // chaining crc32c over segments == one crc32c over their concatenation
+  size_t of = 0, rlen;
+  const void *p;
+  while ((rlen = slice_reader(slice, &p))) {
+    std::memcpy(c->h_stage + of, p, rlen);
+    of += rlen;
+  }
+  uint32_t out = 0;
+  if (crc_staged(c, of, 0u, &out)) fatal("rd_slice_crc32c");
+  return out;
+}
+
+// ------------------------------------------------------------------- LZ4F
+typedef rd_kafka_resp_err_t (*lz4c_fn)(rd_kafka_broker_t *, int, int, rd_slice_t *, void **,
+                                       size_t *);
+
+RDK_API rd_kafka_resp_err_t rd_kafka_lz4_compress(rd_kafka_broker_t *rkb, int proper_hc,
+                                                  int comp_level, rd_slice_t *slice,
+                                                  void **outbuf, size_t *outlenp) {
+  *outbuf = nullptr;
+  if (comp_level >= 3) {
+    // LZ4HC (lz4frame.c:797-805) is not implemented by the engine: hand the
+    // call to the next definition (librdkafka's own) if there is one.
+    lz4c_fn next = reinterpret_cast<lz4c_fn>(dlsym(RTLD_NEXT, "rd_kafka_lz4_compress"));
+    if (next && next != &rd_kafka_lz4_compress)
+      return next(rkb, proper_hc, comp_level, slice, outbuf, outlenp);
+    const void *skip;
+    while (slice_reader(slice, &skip)) {  // consume like the reference would
+    }
+    return RDK_HIP_RESP_ERR__BAD_COMPRESSION;
+  }
+  Ctx *c = ctx_or_die("rd_kafka_lz4_compress");
+  const size_t total = slice_remains(slice);
+  if (ensure_host(c, total ? total : 1)) fatal("rd_kafka_lz4_compress: pinned staging");
+  size_t of = 0, rlen;
+  const void *p;
+  while ((rlen = slice_reader(slice, &p))) {  // rdkafka_lz4.c:390 loop, gathered
+    std::memcpy(c->h_stage + of, p, rlen);
+    of += rlen;
+  }
+  int rc = lz4f_compress_host(c, of, proper_hc, comp_level, outbuf, outlenp);
+  if (rc < -100) return rc;  // rd_kafka_resp_err_t
+  if (rc) fatal("rd_kafka_lz4_compress");
+  return RDK_HIP_RESP_ERR_NO_ERROR;
+}
+
+RDK_API rd_kafka_resp_err_t rd_kafka_lz4_decompress(rd_kafka_broker_t *rkb, int proper_hc,
+                                                    int64_t Offset, char *inbuf, size_t inlen,
+                                                    void **outbuf, size_t *outlenp) {
+  (void)rkb;
+  (void)Offset;
+  *outbuf = nullptr;
+  Ctx *c = ctx_or_die("rd_kafka_lz4_decompress");
+  int rc = lz4f_decompress_host(c, proper_hc, reinterpret_cast<uint8_t *>(inbuf), inlen, outbuf,
+                                outlenp);
+  if (rc < -100) return rc;
+  if (rc) fatal("rd_kafka_lz4_decompress");
+  return RDK_HIP_RESP_ERR_NO_ERROR;
+}

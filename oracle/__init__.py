@@ -1,0 +1,238 @@
+"""CPU oracle for the record-batch hot path -- TEST INFRASTRUCTURE ONLY.
+
+Loads ``oracle/liboracle.so`` (the C restatement in crc32c_oracle.c /
+lz4_oracle.c) and, when it has been built, ``oracle/_ref/libreflz4.so`` (the
+reference's own vendored lz4 1.9.2 + xxHash compiled in place from
+/root/reference/src, driven by ref_glue.c).
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg
+may import this module, and only as the checker / the timed CPU baseline.
+The product package ``librdkafka_amd`` never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_REFLIB = os.path.join(_HERE, "_ref", "libreflz4.so")
+
+ERR_NO_ERROR = 0
+ERR_BAD_MSG = -199
+ERR_BAD_COMPRESSION = -198
+ERR_CRIT_SYS_RESOURCE = -194
+
+
+def build(ref: bool = True) -> None:
+    """Compile the oracle (and, if /root/reference exists, the reference lz4)."""
+    subprocess.run(["make", "-s", "-C", _HERE, "liboracle.so"], check=True)
+    if ref and os.path.isdir("/root/reference/src"):
+        subprocess.run(["make", "-s", "-C", _HERE, "ref"], check=True)
+
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build(ref=False)
+        L = C.CDLL(_LIB)
+        u8p, u32p, u64p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+        L.or_crc32c.restype = C.c_uint32
+        L.or_crc32c.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t]
+        L.or_crc32c_bitwise.restype = C.c_uint32
+        L.or_crc32c_bitwise.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t]
+        L.or_crc32c_hw.restype = C.c_uint32
+        L.or_crc32c_hw.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t]
+        L.or_crc32c_hw_available.restype = C.c_int
+        L.or_crc32c_combine.restype = C.c_uint32
+        L.or_crc32c_combine.argtypes = [C.c_uint32, C.c_uint32, C.c_size_t]
+        L.or_crc32c_batches_mt.restype = None
+        L.or_crc32c_batches_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_size_t, C.c_int]
+        L.or_xxh32.restype = C.c_uint32
+        L.or_xxh32.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32]
+        L.or_lz4_compress_block.restype = C.c_int
+        L.or_lz4_compress_block.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        L.or_lz4_decompress_block.restype = C.c_int
+        L.or_lz4_decompress_block.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        L.or_rdk_lz4_compress.restype = C.c_int
+        L.or_rdk_lz4_compress.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_size_t,
+                                          C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+        L.or_rdk_lz4_decompress.restype = C.c_int
+        L.or_rdk_lz4_decompress.argtypes = [C.c_int, C.c_void_p, C.c_size_t,
+                                            C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+        L.or_lz4f_compress_bound.restype = C.c_size_t
+        L.or_lz4f_compress_bound.argtypes = [C.c_size_t]
+        L.or_free.argtypes = [C.c_void_p]
+        L.or_lz4f_compress_batches_mt.restype = C.c_int
+        L.or_lz4f_compress_batches_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.or_lz4f_decompress_batches_mt.restype = C.c_int
+        L.or_lz4f_decompress_batches_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                    C.c_int]
+        _lib = L
+    return _lib
+
+
+def ref_available() -> bool:
+    return os.path.exists(_REFLIB)
+
+
+def ref():
+    """The reference's own lz4/xxhash build (None if not built)."""
+    global _ref
+    if _ref is None and ref_available():
+        R = C.CDLL(_REFLIB)
+        R.ref_xxh32.restype = C.c_uint32
+        R.ref_xxh32.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32]
+        R.ref_lz4_decompress_safe.restype = C.c_int
+        R.ref_lz4_decompress_safe.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        R.ref_lz4_compress_block.restype = C.c_int
+        R.ref_lz4_compress_block.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        R.ref_rdk_lz4_compress.restype = C.c_int
+        R.ref_rdk_lz4_compress.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_char_p),
+                                           C.POINTER(C.c_size_t), C.c_int,
+                                           C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+        R.ref_rdk_lz4_decompress.restype = C.c_int
+        R.ref_rdk_lz4_decompress.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.c_size_t,
+                                             C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                                             C.POINTER(C.c_int)]
+        R.ref_free.argtypes = [C.c_void_p]
+        _ref = R
+    return _ref
+
+
+def _buf(data: bytes):
+    return C.create_string_buffer(bytes(data), max(1, len(data)))
+
+
+# ---------------------------------------------------------------- oracle API
+def crc32c(crc: int, data: bytes) -> int:
+    b = _buf(data)
+    return lib().or_crc32c(crc, b, len(data))
+
+
+def crc32c_bitwise(crc: int, data: bytes) -> int:
+    b = _buf(data)
+    return lib().or_crc32c_bitwise(crc, b, len(data))
+
+
+def crc32c_hw(crc: int, data: bytes) -> int:
+    b = _buf(data)
+    return lib().or_crc32c_hw(crc, b, len(data))
+
+
+def crc32c_combine(a: int, b: int, len_b: int) -> int:
+    return lib().or_crc32c_combine(a, b, len_b)
+
+
+def xxh32(data: bytes, seed: int = 0) -> int:
+    b = _buf(data)
+    return lib().or_xxh32(b, len(data), seed)
+
+
+def lz4_compress_block(data: bytes, acceleration: int = 1) -> bytes | None:
+    """LZ4F block compression (cap = n-1); None means 'stored raw'."""
+    n = len(data)
+    src = _buf(data)
+    dst = C.create_string_buffer(max(16, n + 16))
+    r = lib().or_lz4_compress_block(src, n, dst, max(0, n - 1), acceleration)
+    return None if r == 0 else dst.raw[:r]
+
+
+def lz4_decompress_block(block: bytes, capacity: int, history: bytes = b"") -> tuple[int, bytes]:
+    buf = C.create_string_buffer(len(history) + capacity + 64)
+    C.memmove(buf, history, len(history))
+    src = _buf(block)
+    dst = C.cast(C.addressof(buf) + len(history), C.c_void_p)
+    r = lib().or_lz4_decompress_block(src, len(block), dst, capacity, len(history))
+    if r < 0:
+        return r, b""
+    return r, buf.raw[len(history):len(history) + r]
+
+
+def rdk_lz4_compress(data: bytes, proper_hc: int = 1, comp_level: int = 0) -> tuple[int, bytes]:
+    src = _buf(data)
+    out = C.c_void_p()
+    n = C.c_size_t()
+    err = lib().or_rdk_lz4_compress(proper_hc, comp_level, src, len(data), C.byref(out), C.byref(n))
+    if err:
+        return err, b""
+    res = C.string_at(out, n.value)
+    lib().or_free(out)
+    return 0, res
+
+
+def rdk_lz4_decompress(frame: bytes, proper_hc: int = 1) -> tuple[int, bytes]:
+    src = _buf(frame)
+    out = C.c_void_p()
+    n = C.c_size_t()
+    err = lib().or_rdk_lz4_decompress(proper_hc, src, len(frame), C.byref(out), C.byref(n))
+    if err:
+        return err, b""
+    res = C.string_at(out, n.value) if n.value else b""
+    lib().or_free(out)
+    return 0, res
+
+
+# ------------------------------------------------------- reference (compiled)
+def ref_rdk_lz4_compress(segments, proper_hc: int = 1, comp_level: int = 0) -> tuple[int, bytes]:
+    if isinstance(segments, (bytes, bytearray)):
+        segments = [bytes(segments)]
+    R = ref()
+    n = len(segments)
+    ptrs = (C.c_char_p * max(1, n))(*[bytes(s) for s in segments])
+    lens = (C.c_size_t * max(1, n))(*[len(s) for s in segments])
+    out = C.c_void_p()
+    olen = C.c_size_t()
+    err = R.ref_rdk_lz4_compress(proper_hc, comp_level, ptrs, lens, n, C.byref(out), C.byref(olen))
+    if err:
+        return err, b""
+    res = C.string_at(out, olen.value)
+    R.ref_free(out)
+    return 0, res
+
+
+def ref_rdk_lz4_decompress(frame: bytes, proper_hc: int = 1,
+                           max_msg_size: int = 1000000) -> tuple[int, bytes, int]:
+    R = ref()
+    src = _buf(frame)
+    out = C.c_void_p()
+    olen = C.c_size_t()
+    grow = C.c_int()
+    err = R.ref_rdk_lz4_decompress(proper_hc, src, len(frame), max_msg_size, C.byref(out),
+                                   C.byref(olen), C.byref(grow))
+    if err:
+        return err, b"", grow.value
+    res = C.string_at(out, olen.value) if olen.value else b""
+    R.ref_free(out)
+    return 0, res, grow.value
+
+
+def ref_lz4_decompress_safe(block: bytes, capacity: int) -> tuple[int, bytes]:
+    R = ref()
+    src = _buf(block)
+    dst = C.create_string_buffer(capacity + 64)
+    r = R.ref_lz4_decompress_safe(src, dst, len(block), capacity)
+    return (r, dst.raw[:r]) if r >= 0 else (r, b"")
+
+
+def ref_lz4_compress_block(data: bytes, acceleration: int = 1) -> bytes | None:
+    R = ref()
+    n = len(data)
+    src = _buf(data)
+    dst = C.create_string_buffer(max(16, n + 16))
+    r = R.ref_lz4_compress_block(src, n, dst, max(0, n - 1), acceleration)
+    return None if r == 0 else dst.raw[:r]
+
+
+def ref_xxh32(data: bytes, seed: int = 0) -> int:
+    b = _buf(data)
+    return ref().ref_xxh32(b, len(data), seed)

@@ -1,0 +1,102 @@
+/*
+ * oracle.h -- CPU restatement of librdkafka's record-batch hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is linked into, loaded by
+ * or called from the product (librdkafka_amd/librdkafka_hip.so).  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it,
+ * and only as the checker / the timed CPU baseline.
+ *
+ * Each function cites the reference file:line it restates
+ * (reference = bluelichen19/librdkafka v1.3.0 with its vendored lz4 1.9.2).
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - CRC32C: crc32c.c depends on the generated ../config.h (rd.h:64) and is
+ *     therefore unbuildable here; the restatement is pinned by the reference's
+ *     own known-answer test (crc32c.c:388-438, 0x7dcde113), the standard check
+ *     value and an independent bit-serial implementation.
+ *   - LZ4 / LZ4F / XXH32: the vendored sources (src/lz4.c, src/lz4frame.c,
+ *     src/xxhash.c) compile standalone; oracle/Makefile builds them from
+ *     /root/reference into oracle/_ref/ and tests/golden/ holds frames made by
+ *     that build.  The restatement below is checked byte-for-byte against it.
+ */
+#ifndef RDK_ORACLE_H
+#define RDK_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- CRC32C (Castagnoli, reflected poly 0x82f63b78) ---------------------- */
+void     or_crc32c_init(void);
+/* crc32c.c:97-134 (slicing-by-8 software path) -- chainable like crc32c(). */
+uint32_t or_crc32c(uint32_t crc, const void *buf, size_t len);
+/* Independent bit-at-a-time definition, used to cross-check the above. */
+uint32_t or_crc32c_bitwise(uint32_t crc, const void *buf, size_t len);
+/* crc32c.c:144-231 generalised: crc(A||B) from crc(A), crc(B), len(B). */
+uint32_t or_crc32c_combine(uint32_t crcA, uint32_t crcB, size_t lenB);
+/* Multi-threaded batch CRC used as the timed CPU baseline (bench.py). */
+void     or_crc32c_batches_mt(const uint8_t *base, const uint64_t *offs,
+                              const uint32_t *lens, uint32_t *out, size_t n,
+                              int threads);
+/* Same batch shape through the SSE4.2 crc32q path restated from
+ * crc32c.c:255-338 (3-way interleave + shift merge); returns 0 when the
+ * host CPU lacks SSE4.2 (caller then uses the table path). */
+int      or_crc32c_hw_available(void);
+uint32_t or_crc32c_hw(uint32_t crc, const void *buf, size_t len);
+
+/* ---- XXH32 (xxhash.c:392, used for the LZ4F header checksum) ------------- */
+uint32_t or_xxh32(const void *p, size_t len, uint32_t seed);
+
+/* ---- LZ4 block codec ----------------------------------------------------- */
+/* LZ4_compress_generic(byU16, limitedOutput, noDict, noDictIssue) on a zeroed
+ * table, as reached from LZ4F_compressBlock (lz4frame.c:764) through
+ * LZ4_compress_fast_extState_fastReset (lz4.c:1211).  Returns the compressed
+ * size, or 0 when the block does not fit in dst_cap (LZ4F stores it raw). */
+int or_lz4_compress_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap,
+                          int acceleration);
+/* LZ4_decompress_safe_usingDict (lz4.c:2307 -> 1654) without a dictionary
+ * (independent blocks) or with `dict_size` bytes of history directly in front
+ * of dst (linked blocks).  Returns decoded size or a negative error. */
+int or_lz4_decompress_block(const uint8_t *src, int csize, uint8_t *dst,
+                            int dst_cap, int dict_size);
+
+/* ---- LZ4F frame ---------------------------------------------------------- */
+/* Error codes returned by the rd_kafka_lz4_* restatements (rdkafka.h:258-268) */
+#define OR_ERR_NO_ERROR            0
+#define OR_ERR__BAD_MSG         (-199)
+#define OR_ERR__BAD_COMPRESSION (-198)
+#define OR_ERR__CRIT_SYS_RESOURCE (-194)
+
+/* rd_kafka_lz4_compress (rdkafka_lz4.c:329-442) with the reference's prefs
+ * {blockIndependent, comp_level}.  Levels >= 3 (LZ4HC) are not restated and
+ * return OR_ERR__BAD_COMPRESSION.  *out is malloc()ed. */
+int or_rdk_lz4_compress(int proper_hc, int comp_level, const uint8_t *src,
+                        size_t len, uint8_t **out, size_t *outlen);
+/* rd_kafka_lz4_decompress (rdkafka_lz4.c:167-317): one frame, trailing bytes
+ * -> BAD_MSG, decode errors -> BAD_COMPRESSION, truncated frame -> the
+ * prefix decoded so far.  May modify in[] when !proper_hc.  *out malloc()ed. */
+int or_rdk_lz4_decompress(int proper_hc, uint8_t *in, size_t inlen,
+                          uint8_t **out, size_t *outlen);
+/* Upper bound used for output buffers (LZ4F_compressBound + 1000). */
+size_t or_lz4f_compress_bound(size_t len);
+void   or_free(void *p);
+
+/* Multi-threaded frame compression / decompression of independent batches
+ * (CPU baseline for the LZ4F legs). Returns 0 on success. */
+int or_lz4f_compress_batches_mt(const uint8_t *base, const uint64_t *offs,
+                                const uint32_t *lens, size_t n,
+                                uint8_t *out, const uint64_t *out_offs,
+                                uint32_t *out_lens, int threads);
+int or_lz4f_decompress_batches_mt(const uint8_t *base, const uint64_t *offs,
+                                  const uint32_t *lens, size_t n,
+                                  uint8_t *out, const uint64_t *out_offs,
+                                  const uint32_t *out_caps, uint32_t *out_lens,
+                                  int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,161 @@
+/*
+ * ref_glue.c -- thin driver that calls the REFERENCE's own vendored LZ4F /
+ * LZ4 / XXH32 sources (compiled in place from /root/reference/src by
+ * oracle/Makefile into oracle/_ref/libreflz4.so).
+ * TEST INFRASTRUCTURE ONLY.
+ *
+ * rdkafka_lz4.c itself cannot be compiled here (it needs rdkafka_int.h and the
+ * generated config.h), so its two entry points are re-driven through the same
+ * public LZ4F calls with the same preferences and the same outer loop:
+ *   ref_rdk_lz4_compress   <- rd_kafka_lz4_compress   (rdkafka_lz4.c:329-442)
+ *   ref_rdk_lz4_decompress <- rd_kafka_lz4_decompress (rdkafka_lz4.c:167-317)
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define LZ4_STATIC_LINKING_ONLY
+#include "lz4.h"
+#include "lz4frame.h"
+#include "xxhash.h"
+
+#define ERR_BAD_MSG (-199)
+#define ERR_BAD_COMPRESSION (-198)
+#define ERR_CRIT_SYS_RESOURCE (-194)
+
+uint32_t ref_xxh32(const void *p, size_t len, uint32_t seed) {
+    return XXH32(p, len, seed);
+}
+
+int ref_lz4_decompress_safe(const char *src, char *dst, int csize, int cap) {
+    return LZ4_decompress_safe(src, dst, csize, cap);
+}
+
+/* One LZ4F block exactly as LZ4F_compressBlock reaches it: a fresh stream
+ * state, fastReset, dstCapacity = srcSize-1 (lz4frame.c:739-773). */
+int ref_lz4_compress_block(const char *src, int n, char *dst, int cap, int accel) {
+    LZ4_stream_t st;
+    LZ4_initStream(&st, sizeof st);
+    return LZ4_compress_fast_extState_fastReset(&st, src, dst, n, cap, accel);
+}
+
+static int break_framing(char *out, size_t outlen) {
+    static const char magic[4] = {0x04, 0x22, 0x4d, 0x18};
+    size_t of = 4;
+    if (outlen < 7 || memcmp(out, magic, 4)) return ERR_BAD_COMPRESSION;
+    uint8_t FLG = (uint8_t)out[of++];
+    of++;
+    if ((FLG >> 3) & 1) of += 8;
+    if (of >= outlen) return ERR_BAD_COMPRESSION;
+    out[of] = (char)((XXH32(out, of, 0) >> 8) & 0xff);
+    return 0;
+}
+
+static int fixup_framing(char *in, size_t inlen) {
+    static const char magic[4] = {0x04, 0x22, 0x4d, 0x18};
+    size_t of = 4;
+    if (inlen < 7 || memcmp(in, magic, 4)) return ERR_BAD_COMPRESSION;
+    uint8_t FLG = (uint8_t)in[of++];
+    of++;
+    if ((FLG >> 3) & 1) of += 8;
+    if (of >= inlen) return ERR_BAD_COMPRESSION;
+    in[of] = (char)((XXH32(in + 4, of - 4, 0) >> 8) & 0xff);
+    return 0;
+}
+
+/* Segments are passed as an iovec-like (ptr,len) list to reproduce the
+ * per-rd_slice-segment LZ4F_compressUpdate calls of rdkafka_lz4.c:390-407. */
+int ref_rdk_lz4_compress(int proper_hc, int comp_level, const char *const *segs,
+                         const size_t *seglens, int nsegs, char **outbuf,
+                         size_t *outlenp) {
+    LZ4F_compressionContext_t cctx;
+    size_t len = 0, out_of = 0, r;
+    for (int i = 0; i < nsegs; i++) len += seglens[i];
+    LZ4F_preferences_t prefs;
+    memset(&prefs, 0, sizeof prefs);
+    prefs.frameInfo.blockMode = LZ4F_blockIndependent;
+    prefs.compressionLevel = comp_level;
+    *outbuf = NULL;
+    size_t out_sz = LZ4F_compressBound(len, NULL) + 1000;
+    char *out = malloc(out_sz);
+    if (!out) return ERR_CRIT_SYS_RESOURCE;
+    if (LZ4F_isError(LZ4F_createCompressionContext(&cctx, LZ4F_VERSION))) {
+        free(out);
+        return ERR_CRIT_SYS_RESOURCE;
+    }
+    int err = 0;
+    r = LZ4F_compressBegin(cctx, out, out_sz, &prefs);
+    if (LZ4F_isError(r)) { err = ERR_BAD_COMPRESSION; goto done; }
+    out_of += r;
+    for (int i = 0; i < nsegs; i++) {
+        if (!seglens[i]) continue;
+        r = LZ4F_compressUpdate(cctx, out + out_of, out_sz - out_of, segs[i], seglens[i], NULL);
+        if (LZ4F_isError(r)) { err = ERR_BAD_COMPRESSION; goto done; }
+        out_of += r;
+    }
+    r = LZ4F_compressEnd(cctx, out + out_of, out_sz - out_of, NULL);
+    if (LZ4F_isError(r)) { err = ERR_BAD_COMPRESSION; goto done; }
+    out_of += r;
+    if (!proper_hc && (err = break_framing(out, out_of))) goto done;
+    *outbuf = out;
+    *outlenp = out_of;
+done:
+    LZ4F_freeCompressionContext(cctx);
+    if (err) free(out);
+    return err;
+}
+
+/* max_msg_size plays the role of rkb->rkb_rk->rk_conf.max_msg_size;
+ * *zbuf_grow counts the x1.75 regrowths (rdkafka_lz4.c:268-286). */
+int ref_rdk_lz4_decompress(int proper_hc, char *inbuf, size_t inlen,
+                           size_t max_msg_size, char **outbuf, size_t *outlenp,
+                           int *zbuf_grow) {
+    LZ4F_decompressionContext_t dctx;
+    LZ4F_frameInfo_t fi;
+    size_t in_sz, out_sz, in_of, out_of, r, est, outlen;
+    int err = 0;
+    char *out = NULL;
+    *outbuf = NULL;
+    *zbuf_grow = 0;
+    if (LZ4F_isError(LZ4F_createDecompressionContext(&dctx, LZ4F_VERSION)))
+        return ERR_CRIT_SYS_RESOURCE;
+    if (!proper_hc && (err = fixup_framing(inbuf, inlen))) goto done;
+    in_sz = inlen;
+    r = LZ4F_getFrameInfo(dctx, &fi, inbuf, &in_sz);
+    if (LZ4F_isError(r)) { err = ERR_BAD_COMPRESSION; goto done; }
+    if (fi.contentSize == 0 || fi.contentSize > inlen * 255)
+        est = inlen * 4 < max_msg_size ? inlen * 4 : max_msg_size;
+    else
+        est = (size_t)fi.contentSize;
+    out = malloc(est ? est : 1);
+    if (!out) { err = ERR_CRIT_SYS_RESOURCE; goto done; }
+    outlen = est;
+    in_of = in_sz;
+    out_of = 0;
+    while (in_of < inlen) {
+        out_sz = outlen - out_of;
+        in_sz = inlen - in_of;
+        r = LZ4F_decompress(dctx, out + out_of, &out_sz, inbuf + in_of, &in_sz, NULL);
+        if (LZ4F_isError(r)) { err = ERR_BAD_COMPRESSION; goto done; }
+        out_of += out_sz;
+        in_of += in_sz;
+        if (r == 0) break;
+        if (out_of == outlen) {
+            size_t extra = outlen * 3 / 4 > 1024 ? outlen * 3 / 4 : 1024;
+            char *tmp;
+            (*zbuf_grow)++;
+            if (!(tmp = realloc(out, outlen + extra))) { err = ERR_CRIT_SYS_RESOURCE; goto done; }
+            out = tmp;
+            outlen += extra;
+        }
+    }
+    if (in_of < inlen) { err = ERR_BAD_MSG; goto done; }
+    *outbuf = out;
+    *outlenp = out_of;
+done:
+    LZ4F_freeDecompressionContext(dctx);
+    if (err && out) free(out);
+    return err;
+}
+
+void ref_free(void *p) { free(p); }

@@ -13,7 +13,7 @@
  *  2. ENGINE batch API (rdk_hip_*).  Device-resident batches of many
  *     toppars' record batches, processed in one launch per stage on a caller
  *     stream.  Plain pointers and sizes only; `stream` is a hipStream_t
- *     passed as void* (NULL = the engine's own per-thread stream).
+ *     passed as void* (NULL = the HIP null stream, as in the HIP API).
  *
  * Every function that touches the GPU fails loudly (returns RDK_HIP_E_* or,
  * for the drop-in symbols, which have no error channel, prints and aborts)

@@ -238,9 +238,14 @@ def _ptr(t):
 
 
 def _stream(stream):
+    """Default to torch's current stream so engine launches are ordered with
+    the torch ops that produce / consume the same device tensors."""
     if stream is None:
-        return None
-    return C.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+        if torch is None:
+            return None
+        stream = torch.cuda.current_stream()
+    h = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    return C.c_void_p(h) if h else None  # 0 -> the null stream
 
 
 def crc32c_ranges(base, offs, lens, out, init=None, stream=None) -> None:

@@ -317,7 +317,7 @@ RDK_API int rdk_hip_crc32c_ranges(const void *d_base, const uint64_t *d_offs,
   if (!c) return RDK_HIP_E_NODEV;
   if (!n) return RDK_HIP_OK;
   if (!d_base || !d_offs || !d_lens || !d_out) return set_error(RDK_HIP_E_INVAL, "null pointer");
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(crc32c_ranges_kernel, dim3(crc_grid(n)), dim3(kCrcBlock), 0, s,
                      static_cast<const uint8_t *>(d_base), d_offs, d_lens, d_init, d_out, n,
                      crc_tables_dev(c->device));
@@ -333,7 +333,7 @@ RDK_API int rdk_hip_msgset_v2_crc(void *d_base, const uint64_t *d_batch_offs,
   if (!n) return RDK_HIP_OK;
   if (!d_base || !d_batch_offs || !d_batch_caps || !d_out)
     return set_error(RDK_HIP_E_INVAL, "null pointer");
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  hipStream_t s = static_cast<hipStream_t>(stream);
   uint8_t *b = static_cast<uint8_t *>(d_base);
   const uint32_t *tab = crc_tables_dev(c->device);
   const dim3 g(crc_grid(n)), blk(kCrcBlock);

@@ -1,0 +1,518 @@
+// lz4_decode.hip -- LZ4F frame decompression on gfx950.
+//
+// Replaces rd_kafka_lz4_decompress (src/rdkafka_lz4.c:167-317) ->
+// LZ4F_decompress (lz4frame.c:1371) -> LZ4_decompress_safe_usingDict
+// (lz4.c:2307 -> LZ4_decompress_generic lz4.c:1654-2068).
+//
+// Pipeline per batch of frames (DESIGN.md "LZ4F decode"):
+//   1. walk kernel   : one lane per frame parses the header and block table
+//                      (FrameWalker, lz4_frame.h) into descriptors;
+//   2. block kernel  : one wavefront per independent block decodes straight
+//                      into out + k*maxBlockSize (zero-copy for regular frames);
+//                      linked frames / frames with more than kMaxDesc blocks
+//                      are decoded whole by one wavefront, in stream order;
+//   3. finish kernel : one wavefront per frame applies the frame-level checks
+//                      (content size / checksum, trailing bytes) in the
+//                      reference's order and compacts irregular frames.
+//
+// The block decoder is a wave-uniform restatement of LZ4_decompress_generic
+// including its fast loop (lz4.c:1707-1824) and the safe-loop shortcut
+// (lz4.c:1846-1889): every bounds check is kept so malformed blocks are
+// accepted or rejected exactly as the reference does.  Control is scalar
+// (token parsing from a 512-byte register window via v_readlane); literal and
+// match bytes are moved by all 64 lanes.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "lz4_device.h"
+#include "lz4_frame.h"
+
+namespace rdk {
+
+constexpr int kMaxDesc = 64;          // descriptors per frame (4 MiB of 64 KiB blocks)
+constexpr int kFastloopSafeDistance = 64;
+
+struct BlockDesc {
+  BlockInfo b;
+  int32_t result;   // decoded bytes, or <0
+  uint32_t pad;
+};
+
+struct FrameState {
+  FrameInfo fi;
+  int32_t seq_result;  // F_SEQ frames: total bytes or <0
+  uint32_t pad;
+};
+
+// ----------------------------------------------------------- input window
+struct InWin {
+  uintptr_t base;  // 4-aligned address held by lane 0 of `cur`
+  uintptr_t lim;   // first address past the last readable dword
+  uint32_t cur, nxt;
+};
+
+__device__ __forceinline__ uint32_t ld_dw(uintptr_t a, uintptr_t lim) {
+  return a < lim ? *(g_cu32 *)a : 0u;
+}
+
+__device__ __forceinline__ void win_load(InWin &w, uintptr_t base, int lane) {
+  w.base = base;
+  w.cur = ld_dw(base + 4u * lane, w.lim);
+  w.nxt = ld_dw(base + 256u + 4u * lane, w.lim);
+}
+
+__device__ __forceinline__ uint32_t win_byte(InWin &w, uintptr_t p, int lane) {
+  if (p < w.base || p >= w.base + 512u) {
+    win_load(w, p & ~uintptr_t(3), lane);
+  } else if (p >= w.base + 256u) {
+    w.base += 256u;
+    w.cur = w.nxt;
+    w.nxt = ld_dw(w.base + 256u + 4u * lane, w.lim);
+  }
+  const uint32_t off = uint32_t(p - w.base);
+  const uint32_t dw = __builtin_amdgcn_readlane(off < 256u ? w.cur : w.nxt, int((off & 255u) >> 2));
+  return (dw >> (8u * uint32_t(p & 3u))) & 0xFFu;
+}
+
+// ---------------------------------------------------------- byte movers
+__device__ __forceinline__ void copy_fwd(uintptr_t d, uintptr_t s, uint32_t len, int lane) {
+  asm volatile("" ::: "memory");
+  for (uint32_t base = 0; base < len; base += 256u) {
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = base + lane + 64u * j;
+      v[j] = i < len ? ldb(s + i) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = base + lane + 64u * j;
+      if (i < len) stb(d + i, v[j]);
+    }
+  }
+  asm volatile("" ::: "memory");
+}
+
+// out[op+i] = out[op-offset+i] with LZ77 overlap semantics
+__device__ __forceinline__ void copy_match(uintptr_t dst, uint32_t op, uint32_t offset,
+                                           uint32_t len, int lane) {
+  asm volatile("" ::: "memory");
+  if (offset == 0) {  // the reference writes zeros (lz4.c:2026 / LZ4_memcpy_using_offset)
+    for (uint32_t i = lane; i < len; i += 64u) stb(dst + op + i, 0u);
+  } else if (offset >= len || offset >= 64u) {
+    // chunks of min(offset, 256) bytes never read bytes written in the same chunk
+    const uint32_t chunk = offset >= 256u ? 256u : (offset >= 64u ? 64u : offset);
+    for (uint32_t base = 0; base < len; base += chunk) {
+      uint32_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = base + lane + 64u * j;
+        v[j] = (lane + 64u * j < chunk && i < len) ? ldb(dst + op - offset + i) : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = base + lane + 64u * j;
+        if (lane + 64u * j < chunk && i < len) stb(dst + op + i, v[j]);
+      }
+      asm volatile("" ::: "memory");
+    }
+  } else {  // small period: out[op+i] = out[op-offset + (i mod offset)]
+    const uint32_t lane_mod = uint32_t(lane) % offset, step_mod = 64u % offset;
+    uint32_t cur = 0;
+    for (uint32_t base = 0; base < len; base += 64u) {
+      uint32_t m = lane_mod + cur;
+      if (m >= offset) m -= offset;
+      const uint32_t i = base + lane;
+      if (i < len) stb(dst + op + i, ldb(dst + op - offset + m));
+      cur += step_mod;
+      if (cur >= offset) cur -= offset;
+    }
+  }
+  asm volatile("" ::: "memory");
+}
+
+// ---------------------------------------------------------- block decoder
+// Returns decoded size, -1 for a block the reference rejects, -2 when the
+// caller's buffer (realcap) is too small.  `hist` = bytes of frame history
+// directly in front of dst (linked frames), selecting noDict /
+// withSmallPrefix / withPrefix64k exactly like LZ4_decompress_safe_usingDict.
+__device__ int decode_block(uintptr_t src, int csize, uintptr_t dst, int vcap, int realcap,
+                            int hist, int lane) {
+  const int iend = csize, oend = vcap;
+  const bool prefix64k = hist >= 65535;
+  const long lowPrefix = hist <= 0 ? 0L : (prefix64k ? -65536L : -long(hist));
+  InWin w;
+  w.lim = (src + uintptr_t(csize) + 3u) & ~uintptr_t(3);
+  win_load(w, src & ~uintptr_t(3), lane);
+#define RDK_B(i) win_byte(w, src + uintptr_t(i), lane)
+  int ip = 0, op = 0, cpy = 0;
+  uint32_t token, length;
+  long match, offset;
+
+  if (oend == 0) return (csize == 1 && RDK_B(0) == 0) ? 0 : -1;
+  if (csize == 0) return -1;
+
+  // read_variable_length (lz4.c:1625): -1 initial error, -2 loop error
+  auto rvl = [&](int lencheck, bool initial_check, uint32_t &len) -> int {
+    uint32_t acc = 0, b;
+    if (initial_check && ip >= lencheck) { len = 0; return -1; }
+    do {
+      b = RDK_B(ip);
+      ip++;
+      acc += b;
+      if (ip >= lencheck) { len = acc; return -2; }
+    } while (b == 255u);
+    len = acc;
+    return 0;
+  };
+  auto lit = [&](uint32_t n) -> bool {
+    if (op + int(n) > realcap) return false;
+    copy_fwd(dst + op, src + ip, n, lane);
+    return true;
+  };
+  auto mat = [&](uint32_t n) -> bool {
+    if (op + int(n) > realcap) return false;
+    copy_match(dst, uint32_t(op), uint32_t(offset), n, lane);
+    return true;
+  };
+
+  if (oend - op < kFastloopSafeDistance) goto safe_decode;
+  for (;;) {  // fast loop (lz4.c:1712-1824)
+    token = RDK_B(ip);
+    ip++;
+    length = token >> 4;
+    if (length == 15u) {
+      uint32_t add;
+      if (rvl(iend - 15, true, add) == -1) return -1;
+      length += add;
+      cpy = op + int(length);
+      if (cpy > oend - 32 || ip + int(length) > iend - 32) goto safe_literal_copy;
+      if (!lit(length)) return -2;
+      ip += int(length);
+      op = cpy;
+    } else {
+      cpy = op + int(length);
+      if (ip > iend - (16 + 1)) goto safe_literal_copy;
+      if (!lit(length)) return -2;
+      ip += int(length);
+      op = cpy;
+    }
+    offset = long(RDK_B(ip)) | (long(RDK_B(ip + 1)) << 8);
+    ip += 2;
+    match = op - offset;
+    length = token & 15u;
+    if (length == 15u) {
+      uint32_t add;
+      if (match < lowPrefix) return -1;
+      if (rvl(iend - kLz4LastLiterals + 1, false, add) != 0) return -1;
+      length += add + kLz4MinMatch;
+      if (op + int(length) >= oend - kFastloopSafeDistance) goto safe_match_copy;
+    } else {
+      length += kLz4MinMatch;
+      if (op + int(length) >= oend - kFastloopSafeDistance) goto safe_match_copy;
+      if ((prefix64k || match >= lowPrefix) && offset >= 8) {
+        if (!mat(length)) return -2;
+        op += int(length);
+        continue;
+      }
+    }
+    if (match < lowPrefix) return -1;
+    if (!mat(length)) return -2;
+    op += int(length);
+  }
+
+safe_decode:
+  for (;;) {  // safe loop (lz4.c:1827-2053)
+    token = RDK_B(ip);
+    ip++;
+    length = token >> 4;
+    if (length != 15u && ip < iend - 16 && op <= oend - 32) {  // shortcut
+      if (!lit(length)) return -2;
+      op += int(length);
+      ip += int(length);
+      length = token & 15u;
+      offset = long(RDK_B(ip)) | (long(RDK_B(ip + 1)) << 8);
+      ip += 2;
+      match = op - offset;
+      if (length != 15u && offset >= 8 && (prefix64k || match >= lowPrefix)) {
+        if (!mat(length + kLz4MinMatch)) return -2;
+        op += int(length) + kLz4MinMatch;
+        continue;
+      }
+      goto copy_match_len;
+    }
+    if (length == 15u) {
+      uint32_t add;
+      if (rvl(iend - 15, true, add) == -1) return -1;
+      length += add;
+    }
+    cpy = op + int(length);
+  safe_literal_copy:
+    if (cpy > oend - kLz4MFLimit || ip + int(length) > iend - (2 + 1 + kLz4LastLiterals)) {
+      if (ip + int(length) != iend || cpy > oend) return -1;
+      if (!lit(length)) return -2;
+      ip += int(length);
+      op += int(length);
+      break;
+    }
+    if (!lit(length)) return -2;
+    ip += int(length);
+    op = cpy;
+    offset = long(RDK_B(ip)) | (long(RDK_B(ip + 1)) << 8);
+    ip += 2;
+    match = op - offset;
+    length = token & 15u;
+  copy_match_len:
+    if (length == 15u) {
+      uint32_t add;
+      if (rvl(iend - kLz4LastLiterals + 1, false, add) != 0) return -1;
+      length += add;
+    }
+    length += kLz4MinMatch;
+  safe_match_copy:
+    if (match < lowPrefix) return -1;
+    cpy = op + int(length);
+    if (cpy > oend - kLz4LastLiterals) return -1;
+    if (!mat(length)) return -2;
+    op = cpy;
+  }
+#undef RDK_B
+  return op;
+}
+
+// ------------------------------------------------------------ kernels
+struct DevReader {
+  uintptr_t p;
+  __device__ uint32_t operator()(uint64_t i) const { return ldb(p + i); }
+};
+
+__global__ void lz4f_walk_kernel(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
+                                 const uint32_t *__restrict__ in_lens, uint32_t n,
+                                 FrameState *__restrict__ fs, BlockDesc *__restrict__ bd) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n) return;
+  FrameWalker<DevReader> wk{DevReader{reinterpret_cast<uintptr_t>(in) + in_offs[f]}, in_lens[f]};
+  wk.header();
+  BlockInfo b;
+  uint32_t k = 0;
+  while (wk.next(b)) {
+    if (k < uint32_t(kMaxDesc)) {
+      bd[size_t(f) * kMaxDesc + k].b = b;
+      bd[size_t(f) * kMaxDesc + k].result = 0;
+    }
+    ++k;
+  }
+  wk.fi.nblocks = k < uint32_t(kMaxDesc) ? k : uint32_t(kMaxDesc);
+  if ((wk.fi.flags & F_LINKED) || k > uint32_t(kMaxDesc)) wk.fi.flags |= F_SEQ;
+  fs[f].fi = wk.fi;
+  fs[f].seq_result = 0;
+}
+
+// one block: raw copy or LZ4 decode, with the block checksum check first
+// (dstage_getCBlock verifies XXH32 before decoding, lz4frame.c:1596-1608)
+__device__ int run_block(const BlockInfo &b, uintptr_t frame, uintptr_t dst, uint32_t max_block,
+                         int realcap, int hist, int lane) {
+  const uintptr_t src = frame + b.src_off;
+  if (b.flags & B_RAW) {
+    if (int(b.csize) > realcap) return -2;
+    copy_fwd(dst, src, b.csize, lane);
+    if (b.flags & B_XXH) {
+      uint32_t h = lane == 0 ? xxh32_lane(src, b.csize, 0) : 0u;
+      if (uni(h) != b.xxh) return -1;
+    }
+    return int(b.csize);
+  }
+  if (b.flags & B_XXH) {
+    uint32_t h = lane == 0 ? xxh32_lane(src, b.csize, 0) : 0u;
+    if (uni(h) != b.xxh) return -1;
+  }
+  return decode_block(src, int(b.csize), dst, int(max_block), realcap, hist, lane);
+}
+
+__device__ __forceinline__ int realcap_at(uint64_t cap, uint64_t at, uint32_t limit) {
+  if (cap <= at) return 0;
+  const uint64_t r = cap - at;
+  return int(r < limit ? r : limit);
+}
+
+// independent blocks of regular frames: one wavefront per (frame, block)
+__global__ __launch_bounds__(256) void lz4f_blocks_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs, uint8_t *out,
+    const uint64_t *__restrict__ out_offs, const uint32_t *__restrict__ out_caps, uint32_t n,
+    const FrameState *__restrict__ fs, BlockDesc *__restrict__ bd) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t gw = blockIdx.x * wpb + uni(threadIdx.x >> 6);
+  const uint64_t items = uint64_t(n) * kMaxDesc;
+  for (uint64_t it = gw; it < items; it += uint64_t(gridDim.x) * wpb) {
+    const uint32_t f = uint32_t(it / kMaxDesc), k = uint32_t(it % kMaxDesc);
+    const uint32_t status = uni(uint32_t(fs[f].fi.status));
+    const uint32_t flags = uni(fs[f].fi.flags);
+    const uint32_t nblocks = uni(fs[f].fi.nblocks);
+    if (status != 0 || (flags & (F_SKIPPABLE | F_SEQ)) || k >= nblocks) continue;
+    const uint32_t mb = uni(fs[f].fi.max_block);
+    const uintptr_t frame = reinterpret_cast<uintptr_t>(in) + in_offs[f];
+    const uintptr_t obase = reinterpret_cast<uintptr_t>(out) + out_offs[f];
+    BlockInfo b = bd[size_t(f) * kMaxDesc + k].b;
+    b.src_off = uni(b.src_off); b.csize = uni(b.csize); b.flags = uni(b.flags); b.xxh = uni(b.xxh);
+    const uint64_t slot = uint64_t(k) * mb;
+    const int r = run_block(b, frame, obase + slot, mb, realcap_at(out_caps[f], slot, mb), 0, lane);
+    if (lane == 0) bd[size_t(f) * kMaxDesc + k].result = r;
+  }
+}
+
+// linked frames and frames with more than kMaxDesc blocks: one wavefront
+// decodes the whole frame in stream order into contiguous output
+__global__ __launch_bounds__(256) void lz4f_seq_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
+    const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
+    const uint32_t *__restrict__ out_caps, uint32_t n, FrameState *__restrict__ fs) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t gw = blockIdx.x * wpb + uni(threadIdx.x >> 6);
+  for (uint32_t f = gw; f < n; f += gridDim.x * wpb) {
+    const uint32_t status = uni(uint32_t(fs[f].fi.status));
+    const uint32_t flags = uni(fs[f].fi.flags);
+    if (status != 0 || (flags & F_SKIPPABLE) || !(flags & F_SEQ)) continue;
+    const uintptr_t frame = reinterpret_cast<uintptr_t>(in) + in_offs[f];
+    const uintptr_t obase = reinterpret_cast<uintptr_t>(out) + out_offs[f];
+    const uint64_t cap = out_caps[f];
+    FrameWalker<DevReader> wk{DevReader{frame}, in_lens[f]};
+    wk.header();
+    const uint32_t mb = uni(wk.fi.max_block);
+    const bool linked = flags & F_LINKED;
+    uint64_t produced = 0;
+    int32_t res = 0;
+    BlockInfo b;
+    while (wk.next(b)) {
+      b.src_off = uni(b.src_off); b.csize = uni(b.csize); b.flags = uni(b.flags); b.xxh = uni(b.xxh);
+      const int hist = linked ? int(produced < 65536u ? produced : 65536u) : 0;
+      const int r = run_block(b, frame, obase + produced, mb, realcap_at(cap, produced, mb), hist,
+                              lane);
+      if (r < 0) { res = r; break; }
+      produced += uint64_t(r);
+    }
+    if (lane == 0) fs[f].seq_result = res < 0 ? res : int32_t(produced);
+  }
+}
+
+// frame-level verdict + compaction of irregular frames, one wavefront per frame
+__global__ __launch_bounds__(256) void lz4f_finish_kernel(
+    uint8_t *out, const uint64_t *__restrict__ out_offs, uint32_t n,
+    const FrameState *__restrict__ fs, const BlockDesc *__restrict__ bd,
+    uint32_t *__restrict__ out_lens, int32_t *__restrict__ st) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t gw = blockIdx.x * wpb + uni(threadIdx.x >> 6);
+  for (uint32_t f = gw; f < n; f += gridDim.x * wpb) {
+    const FrameInfo fi = fs[f].fi;
+    int32_t status = int32_t(uni(uint32_t(fi.status)));
+    const uint32_t flags = uni(fi.flags);
+    uint64_t total = 0;
+    const uintptr_t obase = reinterpret_cast<uintptr_t>(out) + out_offs[f];
+    if (status == 0 && !(flags & F_SKIPPABLE)) {
+      if (flags & F_SEQ) {
+        const int32_t r = int32_t(uni(uint32_t(fs[f].seq_result)));
+        if (r < 0) status = (r == -2) ? kErrDstSize : kErrBadCompression;
+        else total = uint32_t(r);
+      } else {
+        const uint32_t nb = uni(fi.nblocks), mb = uni(fi.max_block);
+        bool regular = true;
+        for (uint32_t k = 0; k < nb && status == 0; ++k) {
+          const int32_t r = int32_t(uni(uint32_t(bd[size_t(f) * kMaxDesc + k].result)));
+          if (r < 0) { status = (r == -2) ? kErrDstSize : kErrBadCompression; break; }
+          if (k + 1 < nb && uint32_t(r) != mb) regular = false;
+          total += uint32_t(r);
+        }
+        if (status == 0 && !regular) {  // memmove blocks down into stream order
+          uint64_t at = 0;
+          for (uint32_t k = 0; k < nb; ++k) {
+            const uint32_t r = uni(uint32_t(bd[size_t(f) * kMaxDesc + k].result));
+            const uint64_t from = uint64_t(k) * mb;
+            if (from != at) {
+              for (uint32_t base = 0; base < r; base += 256u) {
+                uint32_t v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  const uint32_t i = base + lane + 64u * j;
+                  v[j] = i < r ? ldb(obase + from + i) : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  const uint32_t i = base + lane + 64u * j;
+                  if (i < r) stb(obase + at + i, v[j]);
+                }
+                asm volatile("" ::: "memory");
+              }
+            }
+            at += r;
+          }
+        }
+      }
+      if (status == 0 && (flags & F_ENDMARK)) {  // dstage_getSuffix (lz4frame.c:1694-1731)
+        if ((flags & F_CSIZE) && total != fi.content_size) status = kErrBadCompression;
+        else if (flags & F_CCHK_PRESENT) {
+          asm volatile("" ::: "memory");
+          uint32_t h = lane == 0 ? xxh32_lane(obase, total, 0) : 0u;
+          if (uni(h) != fi.content_xxh) status = kErrBadCompression;
+        }
+      }
+      if (status == 0 && (flags & F_TRAILING)) status = kErrBadMsg;  // rdkafka_lz4.c:291
+    }
+    if (lane == 0) {
+      out_lens[f] = status == 0 ? uint32_t(total) : 0u;
+      st[f] = status;
+    }
+  }
+}
+
+// ------------------------------------------------------------ host side
+static unsigned grid_waves(uint64_t waves, uint32_t wpb) {
+  uint64_t b = (waves + wpb - 1) / wpb;
+  if (b > 8192u) b = 8192u;
+  return b ? unsigned(b) : 1u;
+}
+
+int lz4f_decompress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
+                           const uint32_t *d_in_lens, uint8_t *d_out,
+                           const uint64_t *d_out_offs, const uint32_t *d_out_caps,
+                           uint32_t *d_out_lens, int32_t *d_status, uint32_t n, hipStream_t s) {
+  if (!n) return 0;
+  const size_t fs_bytes = (size_t(n) * sizeof(FrameState) + 255) & ~size_t(255);
+  const size_t bd_bytes = size_t(n) * kMaxDesc * sizeof(BlockDesc);
+  int rc = ensure_dev(c, 1, fs_bytes + bd_bytes);
+  if (rc) return rc;
+  FrameState *fs = reinterpret_cast<FrameState *>(c->d_stage[1]);
+  BlockDesc *bd = reinterpret_cast<BlockDesc *>(c->d_stage[1] + fs_bytes);
+  hipLaunchKernelGGL(lz4f_walk_kernel, dim3((n + 63) / 64), dim3(64), 0, s, d_in, d_in_offs,
+                     d_in_lens, n, fs, bd);
+  hipLaunchKernelGGL(lz4f_blocks_kernel, dim3(grid_waves(uint64_t(n) * kMaxDesc, 4)), dim3(256), 0,
+                     s, d_in, d_in_offs, d_out, d_out_offs, d_out_caps, n, fs, bd);
+  hipLaunchKernelGGL(lz4f_seq_kernel, dim3(grid_waves(n, 4)), dim3(256), 0, s, d_in, d_in_offs,
+                     d_in_lens, d_out, d_out_offs, d_out_caps, n, fs);
+  hipLaunchKernelGGL(lz4f_finish_kernel, dim3(grid_waves(n, 4)), dim3(256), 0, s, d_out,
+                     d_out_offs, n, fs, bd, d_out_lens, d_status);
+  RDK_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace rdk
+
+using namespace rdk;
+
+RDK_API int rdk_hip_lz4f_decompress(const void *d_in, const uint64_t *d_in_offs,
+                                    const uint32_t *d_in_lens, void *d_out,
+                                    const uint64_t *d_out_offs, const uint32_t *d_out_caps,
+                                    uint32_t *d_out_lens, int32_t *d_status, uint32_t n,
+                                    void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_in || !d_in_offs || !d_in_lens || !d_out || !d_out_offs || !d_out_caps || !d_out_lens ||
+      !d_status)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return lz4f_decompress_device(c, static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
+                                static_cast<uint8_t *>(d_out), d_out_offs, d_out_caps, d_out_lens,
+                                d_status, n, s);
+}

@@ -63,7 +63,7 @@ RDK_API int rdk_hip_gen_v2_batches(void *d_base, uint32_t n, uint32_t batch_size
   Ctx *c = ctx();
   if (!c) return RDK_HIP_E_NODEV;
   if (batch_size < 61 || (batch_size & 7)) return set_error(RDK_HIP_E_INVAL, "batch_size");
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  hipStream_t s = static_cast<hipStream_t>(stream);
   const uint64_t nwords = uint64_t(n) * batch_size / 8;
   hipLaunchKernelGGL(fill_random_kernel, dim3(4096), dim3(256), 0, s,
                      static_cast<uint64_t *>(d_base), nwords, seed);

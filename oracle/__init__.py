@@ -105,6 +105,10 @@ def ref():
                                              C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
                                              C.POINTER(C.c_int)]
         R.ref_free.argtypes = [C.c_void_p]
+        R.ref_lz4f_compress_prefs.restype = C.c_int
+        R.ref_lz4f_compress_prefs.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                              C.c_int, C.c_int, C.c_int, C.c_size_t,
+                                              C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
         _ref = R
     return _ref
 
@@ -236,3 +240,19 @@ def ref_lz4_compress_block(data: bytes, acceleration: int = 1) -> bytes | None:
 def ref_xxh32(data: bytes, seed: int = 0) -> int:
     b = _buf(data)
     return ref().ref_xxh32(b, len(data), seed)
+
+
+def ref_lz4f_compress_prefs(data: bytes, linked=0, block_size_id=4, block_checksum=0,
+                            content_checksum=0, content_size=0, level=0, flush_every=0) -> bytes:
+    """A frame from the reference LZ4F encoder with non-default preferences."""
+    R = ref()
+    src = _buf(data)
+    out = C.c_void_p()
+    n = C.c_size_t()
+    err = R.ref_lz4f_compress_prefs(src, len(data), linked, block_size_id, block_checksum,
+                                    content_checksum, content_size, level, flush_every,
+                                    C.byref(out), C.byref(n))
+    assert err == 0, err
+    res = C.string_at(out, n.value)
+    R.ref_free(out)
+    return res

@@ -159,3 +159,52 @@ done:
 }
 
 void ref_free(void *p) { free(p); }
+
+/* Frames with non-default preferences (linked blocks, larger blocks, block /
+ * content checksums, content size, small flushed blocks) made by the
+ * reference LZ4F encoder, to exercise every decode path.  `flush_every` > 0
+ * calls LZ4F_flush after each chunk of that many bytes (irregular blocks). */
+int ref_lz4f_compress_prefs(const char *src, size_t len, int block_linked, int block_size_id,
+                            int block_checksum, int content_checksum, int content_size,
+                            int level, size_t flush_every, char **outbuf, size_t *outlenp) {
+    LZ4F_compressionContext_t cctx;
+    LZ4F_preferences_t prefs;
+    size_t out_of = 0, r;
+    memset(&prefs, 0, sizeof prefs);
+    prefs.frameInfo.blockMode = block_linked ? LZ4F_blockLinked : LZ4F_blockIndependent;
+    prefs.frameInfo.blockSizeID = (LZ4F_blockSizeID_t)block_size_id;
+    prefs.frameInfo.blockChecksumFlag = block_checksum ? LZ4F_blockChecksumEnabled : LZ4F_noBlockChecksum;
+    prefs.frameInfo.contentChecksumFlag = content_checksum ? LZ4F_contentChecksumEnabled : LZ4F_noContentChecksum;
+    prefs.frameInfo.contentSize = content_size ? len : 0;
+    prefs.compressionLevel = level;
+    size_t out_sz = LZ4F_compressBound(len, &prefs) * 2 + 4096 + (flush_every ? (len / flush_every + 1) * 16 : 0);
+    char *out = malloc(out_sz);
+    *outbuf = NULL;
+    if (!out) return ERR_CRIT_SYS_RESOURCE;
+    if (LZ4F_isError(LZ4F_createCompressionContext(&cctx, LZ4F_VERSION))) { free(out); return ERR_CRIT_SYS_RESOURCE; }
+    int err = 0;
+    r = LZ4F_compressBegin(cctx, out, out_sz, &prefs);
+    if (LZ4F_isError(r)) { err = ERR_BAD_COMPRESSION; goto done; }
+    out_of += r;
+    size_t step = flush_every ? flush_every : (len ? len : 1);
+    for (size_t pos = 0; pos < len; pos += step) {
+        size_t n = len - pos < step ? len - pos : step;
+        r = LZ4F_compressUpdate(cctx, out + out_of, out_sz - out_of, src + pos, n, NULL);
+        if (LZ4F_isError(r)) { err = ERR_BAD_COMPRESSION; goto done; }
+        out_of += r;
+        if (flush_every) {
+            r = LZ4F_flush(cctx, out + out_of, out_sz - out_of, NULL);
+            if (LZ4F_isError(r)) { err = ERR_BAD_COMPRESSION; goto done; }
+            out_of += r;
+        }
+    }
+    r = LZ4F_compressEnd(cctx, out + out_of, out_sz - out_of, NULL);
+    if (LZ4F_isError(r)) { err = ERR_BAD_COMPRESSION; goto done; }
+    out_of += r;
+    *outbuf = out;
+    *outlenp = out_of;
+done:
+    LZ4F_freeCompressionContext(cctx);
+    if (err) free(out);
+    return err;
+}

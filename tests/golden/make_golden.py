@@ -156,7 +156,59 @@ def main() -> None:
         err, out, _ = O.ref_rdk_lz4_decompress(f, max_msg_size=1 << 30)
         cases.append({"hex": f.hex(), "err": err, "out_len": len(out), "out_sha256": sha(out)})
     json.dump(cases, open(os.path.join(HERE, "lz4f_decode_cases.json"), "w"))
-    print(f"wrote {len(vecs)} crc vectors, {len(frames)} frames, {len(cases)} decode cases")
+
+    # ---- frames with non-default LZ4F preferences (other producers: linked
+    # blocks, 256 KB blocks, checksums, content size, flushed small blocks),
+    # and mutated copies described as edits of the base frame
+    data = W.gen_json(40000, 5)
+    variants = {
+        "linked": dict(linked=1),
+        "bsid5": dict(block_size_id=5),
+        "checksums_csize": dict(block_checksum=1, content_checksum=1, content_size=1),
+        "flush3000": dict(flush_every=3000),
+        "linked_flush_bchk": dict(linked=1, flush_every=2500, block_checksum=1),
+        "raw_random_cchk": dict(content_checksum=1),
+    }
+    rb = random.Random(5)
+    var = {"input": "gen_json(40000, 5)", "input_sha256": sha(data), "frames": {}, "cases": []}
+    rnd = random.Random(8)
+    for name, kw in variants.items():
+        src = bytes(rb.getrandbits(8) for _ in range(20000)) if name.startswith("raw") else data
+        fr = O.ref_lz4f_compress_prefs(src, **kw)
+        fn = f"variant_{name}.lz4"
+        open(os.path.join(HERE, fn), "wb").write(fr)
+        err, out, _ = O.ref_rdk_lz4_decompress(fr, max_msg_size=1 << 30)
+        assert err == 0 and out == src
+        var["frames"][name] = {"file": fn, "payload_sha256": sha(out), "payload_len": len(out)}
+        for i in range(25):
+            edit = {"base": name}
+            kind = i % 4
+            if kind == 0:
+                edit["flip"] = [[rnd.randrange(7, len(fr)), rnd.getrandbits(8)] for _ in range(2)]
+            elif kind == 1:
+                edit["truncate"] = rnd.randrange(0, len(fr))
+            elif kind == 2:
+                edit["append"] = bytes(rnd.getrandbits(8) for _ in range(3)).hex()
+            else:
+                edit["flip"] = [[rnd.randrange(len(fr) - 12, len(fr)), rnd.getrandbits(8)]]
+            f = apply_edit(fr, edit)
+            err, out, _ = O.ref_rdk_lz4_decompress(f, max_msg_size=1 << 30)
+            edit.update({"err": err, "out_len": len(out), "out_sha256": sha(out)})
+            var["cases"].append(edit)
+    json.dump(var, open(os.path.join(HERE, "lz4f_variants.json"), "w"), indent=0)
+    print(f"wrote {len(vecs)} crc vectors, {len(frames)} frames, {len(cases)} decode cases, "
+          f"{len(var['cases'])} variant cases")
+
+
+def apply_edit(frame: bytes, edit: dict) -> bytes:
+    f = bytearray(frame)
+    for pos, val in edit.get("flip", []):
+        f[pos] = val
+    if "truncate" in edit:
+        f = f[:edit["truncate"]]
+    if "append" in edit:
+        f += bytes.fromhex(edit["append"])
+    return bytes(f)
 
 
 if __name__ == "__main__":

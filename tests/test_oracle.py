@@ -147,3 +147,29 @@ def test_frame_segmentation_independent(oracle_mod):
     cuts = sorted(rnd.sample(range(1, len(data)), 7))
     segs = [data[a:b] for a, b in zip([0] + cuts, cuts + [len(data)])]
     assert oracle_mod.ref_rdk_lz4_compress(segs)[1] == oracle_mod.rdk_lz4_compress(data)[1]
+
+
+def _apply_edit(frame, edit):
+    f = bytearray(frame)
+    for pos, val in edit.get("flip", []):
+        f[pos] = val
+    if "truncate" in edit:
+        f = f[:edit["truncate"]]
+    if "append" in edit:
+        f += bytes.fromhex(edit["append"])
+    return bytes(f)
+
+
+def test_lz4f_variant_frames_match_reference_golden(oracle_mod, golden):
+    """Frames from other producers (linked blocks, 256 KB blocks, checksums,
+    content size, flushed small blocks) and edits of them."""
+    var = golden("lz4f_variants.json")
+    frames = {k: golden(v["file"]) for k, v in var["frames"].items()}
+    for k, v in var["frames"].items():
+        err, out = oracle_mod.rdk_lz4_decompress(frames[k])
+        assert err == 0 and sha(out) == v["payload_sha256"], k
+    for c in var["cases"]:
+        err, out = oracle_mod.rdk_lz4_decompress(_apply_edit(frames[c["base"]], c))
+        assert err == c["err"], c
+        if err == 0:
+            assert len(out) == c["out_len"] and sha(out) == c["out_sha256"], c

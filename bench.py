@@ -113,6 +113,115 @@ def bench_crc(args, rank, world):
     return res
 
 
+# ---------------------------------------------------------------- LZ4F legs
+JSON_BATCH = 1 << 20          # configs[3]/[4]: 1 MiB record batches
+
+
+def _timed(fn, steps, warmup, world):
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        fn()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    barrier(world)
+    return wall * 1e3 / steps, ev0.elapsed_time(ev1) / steps
+
+
+def json_batches(n, size=JSON_BATCH, seed=42):
+    """n device-resident 1 MiB batches of JSON-like records (8 distinct MiB
+    rotated: generation cost stays off the GPU clock, contents stay realistic)."""
+    import torch
+    import librdkafka_amd as L
+    distinct = 8
+    host = L.gen_json(size * distinct, seed)
+    base = torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda()
+    buf = torch.empty(n * size + 256, dtype=torch.uint8, device="cuda")
+    for i in range(n):
+        j = i % distinct
+        buf[i * size:(i + 1) * size] = base[j * size:(j + 1) * size]
+    offs = torch.arange(n, dtype=torch.int64, device="cuda") * size
+    lens = torch.full((n,), size, dtype=torch.int32, device="cuda")
+    return buf, offs, lens
+
+
+def bench_lz4c(args, rank, world, n=None):
+    """configs[2]: LZ4F compress (rd_kafka_lz4_compress semantics) of 1 MiB
+    JSON batches, frames byte-identical to the reference's."""
+    import torch
+    import librdkafka_amd as L
+    n = n or args.partitions // world
+    src, offs, lens = json_batches(n, seed=42 + rank)
+    bound = (L.lz4f_compress_bound(JSON_BATCH) + 255) // 256 * 256
+    dst = torch.empty(n * bound + 256, dtype=torch.uint8, device="cuda")
+    ooffs = torch.arange(n, dtype=torch.int64, device="cuda") * bound
+    olens = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ms, kms = _timed(lambda: L.lz4f_compress_batch(src, offs, lens, dst, ooffs, olens),
+                     args.steps, args.warmup, world)
+    clen = int(olens.sum())
+    return {"ms": ms, "kernel_ms": kms, "bytes": n * JSON_BATCH, "records": n,
+            "alg_bytes": n * JSON_BATCH + clen, "ratio": n * JSON_BATCH / clen,
+            "frames": (dst, ooffs, olens)}
+
+
+def bench_consumer(args, rank, world, n=None):
+    """configs[3]: consumer path per fetched v2 batch: CRC32C verify
+    (check.crcs, rdkafka_msgset_reader.c:982-1015) then LZ4F decompress
+    (rdkafka_msgset_reader.c:393-407) of 1 MiB-record batches."""
+    import numpy as np
+    import torch
+    import librdkafka_amd as L
+    from librdkafka_amd import workload as W
+    n = n or args.partitions // world
+    c = bench_lz4c(argparse.Namespace(steps=1, warmup=0, partitions=n * world), rank, world, n)
+    frames, foffs, flens = c["frames"]
+    fl = flens.cpu().numpy().astype(np.int64)
+    slot = (61 + int(fl.max()) + 255) // 256 * 256
+    batches = torch.zeros(n * slot + 256, dtype=torch.uint8, device="cuda")
+    fo = foffs.cpu().numpy()
+    hdrs = bytearray()
+    for i in range(n):  # v2 header: Length, Attributes = LZ4 (3), RecordCount
+        h = bytearray(W.v2_header(i, 64))
+        h[8:12] = int(61 + fl[i] - 12).to_bytes(4, "big")
+        h[21:23] = (3).to_bytes(2, "big")
+        hdrs += h
+        batches[i * slot + 61:i * slot + 61 + fl[i]] = frames[fo[i]:fo[i] + fl[i]]
+    hd = torch.frombuffer(hdrs, dtype=torch.uint8).cuda().view(n, 61)
+    batches[:n * slot].view(n, slot)[:, :61] = hd
+    boffs = torch.arange(n, dtype=torch.int64, device="cuda") * slot
+    bcaps = torch.full((n,), slot, dtype=torch.int32, device="cuda")
+    crc_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    L.msgset_v2_crc(batches, boffs, bcaps, crc_out, L.V2_CRC_FINALIZE)
+    pay_offs = boffs + 61
+    pay_lens = flens.clone()
+    out = torch.empty(n * JSON_BATCH + 256, dtype=torch.uint8, device="cuda")
+    ooffs = torch.arange(n, dtype=torch.int64, device="cuda") * JSON_BATCH
+    ocaps = torch.full((n,), JSON_BATCH, dtype=torch.int32, device="cuda")
+    olens = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+
+    def step():
+        L.msgset_v2_crc(batches, boffs, bcaps, crc_out, L.V2_CRC_VERIFY)
+        L.lz4f_decompress_batch(batches, pay_offs, pay_lens, out, ooffs, ocaps, olens, st)
+
+    ms, kms = _timed(step, args.steps, args.warmup, world)
+    assert int(crc_out.abs().sum()) == 0 and int(st.abs().sum()) == 0
+    src, _, _ = json_batches(min(n, 8), seed=42 + rank)
+    assert torch.equal(out[:min(n, 8) * JSON_BATCH], src[:min(n, 8) * JSON_BATCH])
+    csum = int(fl.sum())
+    return {"ms": ms, "kernel_ms": kms, "bytes": n * JSON_BATCH, "records": n,
+            "alg_bytes": csum + (csum + 61 * n) + n * JSON_BATCH}
+
+
 def cpu_baseline_crc(buf, n, size, seconds=8.0):
     """The oracle's restatement of crc32c_hw (crc32c.c:255-338, SSE4.2 3-way),
     on CPU_THREADS host threads over a bounded 1 GiB sample of the batches."""
@@ -142,15 +251,69 @@ def cpu_baseline_crc(buf, n, size, seconds=8.0):
                       f", {cpu_model()}"}
 
 
+def cpu_baseline_lz4(kind, n=64, seconds=4.0):
+    """Oracle restatement of rd_kafka_lz4_compress / _decompress (the
+    reference's lz4 1.9.2 LZ4F path, byte-identical output) on CPU_THREADS
+    host threads over n x 1 MiB JSON batches."""
+    import numpy as np
+    import oracle
+    import librdkafka_amd as L
+    data = np.frombuffer(L.gen_json(JSON_BATCH * 8, 42), dtype=np.uint8)
+    src = np.concatenate([data] * (n // 8))
+    offs = (np.arange(n, dtype=np.uint64) * JSON_BATCH).astype(np.uint64)
+    lens = np.full(n, JSON_BATCH, dtype=np.uint32)
+    bound = int(oracle.lib().or_lz4f_compress_bound(JSON_BATCH))
+    cbuf = np.zeros(n * bound, dtype=np.uint8)
+    coffs = (np.arange(n, dtype=np.uint64) * bound).astype(np.uint64)
+    clens = np.zeros(n, dtype=np.uint32)
+    lib = oracle.lib()
+    comp = lambda: lib.or_lz4f_compress_batches_mt(  # noqa: E731
+        src.ctypes.data, offs.ctypes.data, lens.ctypes.data, n, cbuf.ctypes.data,
+        coffs.ctypes.data, clens.ctypes.data, CPU_THREADS)
+    comp()
+    dbuf = np.zeros(n * JSON_BATCH, dtype=np.uint8)
+    dlens = np.zeros(n, dtype=np.uint32)
+    dec = lambda: lib.or_lz4f_decompress_batches_mt(  # noqa: E731
+        cbuf.ctypes.data, coffs.ctypes.data, clens.ctypes.data, n, dbuf.ctypes.data,
+        offs.ctypes.data, lens.ctypes.data, dlens.ctypes.data, CPU_THREADS)
+    fn = comp if kind == "compress" else dec
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(passes * n * JSON_BATCH / el / 1e9, 3), "unit": "GB/s",
+            "cores": CPU_THREADS, "kind": "port",
+            "sample": f"{n} x 1 MiB JSON batches, {passes} passes, rd_kafka_lz4_{kind} restated, "
+                      f"{cpu_model()}"}
+
+
+def leg_line(name, res, steps, world, cpu=None):
+    ach = res["alg_bytes"] / (res["kernel_ms"] / 1e3) / 1e9
+    d = {"GB_per_s": round(res["bytes"] * world / (res["ms"] / 1e3) / 1e9, 2),
+         "ms_per_step": round(res["ms"], 3), "batches": res["records"] * world,
+         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
+    if "ratio" in res:
+        d["compression_ratio"] = round(res["ratio"], 3)
+    if cpu:
+        d["cpu_baseline"] = cpu
+    return d
+
+
 # ------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="crc", choices=["crc"])
+    ap.add_argument("--workload", default="crc", choices=["crc", "lz4c", "consumer"])
     ap.add_argument("--batches", type=int, default=CRC_BATCHES)
+    ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-legs", action="store_true")
     args = ap.parse_args()
 
     rank, local_rank, world = dist_env()
@@ -163,6 +326,22 @@ def main():
     if not os.path.exists(L.LIB_PATH):
         L.build()
     L.init(local_rank)
+
+    if args.workload != "crc":
+        res = bench_lz4c(args, rank, world) if args.workload == "lz4c" else \
+            bench_consumer(args, rank, world)
+        t_max = max_over_ranks(res["ms"], world)
+        if rank == 0:
+            cpu = None
+            if not args.no_cpu_baseline and world == 1:
+                cpu = cpu_baseline_lz4("compress" if args.workload == "lz4c" else "decompress")
+            res["ms"] = t_max
+            print(json.dumps({"workload": args.workload, "n_gpus": world, "steps": args.steps,
+                              **leg_line(args.workload, res, args.steps, world, cpu)}), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
 
     res = bench_crc(args, rank, world)
     # whole-job time per step: max over ranks of the host clock around the
@@ -199,6 +378,17 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             buf, n, size = res["host_sample"]
             line["cpu_baseline"] = cpu_baseline_crc(buf, n, size)
+        del res
+        if not args.no_legs and world == 1:
+            # the LZ4F legs of the same path (configs[2], configs[3]) at 256 x 1 MiB
+            sub = argparse.Namespace(steps=3, warmup=1, partitions=256)
+            cpu = (lambda k: None) if args.no_cpu_baseline else cpu_baseline_lz4
+            line["legs"] = {
+                "lz4f_compress_1MiB_json": leg_line("lz4c", bench_lz4c(sub, rank, world), 3, 1,
+                                                    cpu("compress")),
+                "consumer_crc_verify_lz4f_decompress_1MiB": leg_line(
+                    "consumer", bench_consumer(sub, rank, world), 3, 1, cpu("decompress")),
+            }
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -8,8 +8,13 @@
 //   * one wavefront per byte range (a record batch), persistent grid;
 //   * lane l of iteration k owns the 16-byte vector at V + 1024k + 16l, so
 //     every global_load_dwordx4 of the wave reads 1 KiB contiguous (coalesced);
-//   * a lane folds its vectors into a raw CRC register with 16 slicing-table
-//     lookups + a 4-lookup "advance 1024 bytes" operator (tables in LDS);
+//   * v2 (default): a lane advances its raw CRC register over the 1008-byte
+//     gap with an 8-lookup operator, then absorbs its 16 bytes with two
+//     slicing-by-8 steps (crc32c.c:110-125).  Every byte lookup is split into
+//     two nibble lookups in 32-fold replicated tables (one copy per LDS bank)
+//     so the random table reads are bank-conflict free;
+//   * v1 (RDK_HIP_CRC_V1=1): 16 byte slicing tables + 4-lookup 1024-byte
+//     operator; measured LDS-conflict bound (profiles/r01_crc_v1_*);
 //   * the 64 lane registers are merged by a 6-level xor-shuffle tree whose
 //     level m applies the "advance 16*2^m bytes" operator -- the GF(2)
 //     combine of crc32c.c:144-231 generalised from 3 streams to 64 lanes;
@@ -21,9 +26,13 @@
 #include "common.h"
 #include "crc32c_tables.h"
 
+#include <cstdlib>
+
 namespace rdk {
 
-constexpr int kCrcBlock = 512;       // threads per workgroup (8 waves)
+// threads per workgroup: v2's 73 KiB of tables fit twice per CU -> 2 x 16 waves;
+// v1's 40 KiB fit four times -> 4 x 8 waves
+template <int V> constexpr int crc_block() { return V == 2 ? 1024 : 512; }
 constexpr int kCrcSmall = 64;        // ranges shorter than this: serial lane
 constexpr uint32_t kCrcChunk = 65536; // split of long single ranges
 
@@ -149,10 +158,116 @@ __device__ __attribute__((always_inline)) uint32_t wave_crc(uintptr_t s, uintptr
   return final ? ~x : x;
 }
 
-__device__ __forceinline__ void load_tables(uint32_t *L, const uint32_t *g) {
+
+// ---------------------------------------------------------------- v2 path
+__device__ __forceinline__ uint32_t nib(const lds_u32 *L, int table, uint32_t x, int sh,
+                                        uint32_t lc) {
+  // (nibble << 5) | lane%32: the two fields never overlap, so v_and_or_b32
+  return L[table + int((((x >> sh) & 15u) << 5) | lc)];
+}
+
+// slicing-by-8 on the 8 bytes (s, w): s bytes use T7..T4, w bytes T3..T0
+__device__ __forceinline__ uint32_t step8(const lds_u32 *L, uint32_t s, uint32_t w, uint32_t lc) {
+  uint32_t a = 0, b = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a ^= nib(L, kNibSlice + (2 * (7 - q)) * kNibTable, s, 8 * q, lc) ^
+         nib(L, kNibSlice + (2 * (7 - q) + 1) * kNibTable, s, 8 * q + 4, lc);
+    b ^= nib(L, kNibSlice + (2 * (3 - q)) * kNibTable, w, 8 * q, lc) ^
+         nib(L, kNibSlice + (2 * (3 - q) + 1) * kNibTable, w, 8 * q + 4, lc);
+  }
+  return a ^ b;
+}
+
+__device__ __forceinline__ uint32_t shift1008(const lds_u32 *L, uint32_t x, uint32_t lc) {
+  uint32_t a = 0, b = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    a ^= nib(L, kNibShift + j * kNibTable, x, 4 * j, lc);
+    b ^= nib(L, kNibShift + (j + 1) * kNibTable, x, 4 * j + 4, lc);
+  }
+  return a ^ b;
+}
+
+__device__ __forceinline__ uint32_t shift_tree(const lds_u32 *L, int m, uint32_t x) {
+  const int t = kV2Tree + m * 1024;
+  return L[t + int(x & 0xffu)] ^ L[t + 256 + int((x >> 8) & 0xffu)] ^
+         L[t + 512 + int((x >> 16) & 0xffu)] ^ L[t + 768 + int(x >> 24)];
+}
+
+__device__ __attribute__((always_inline)) uint32_t wave_crc_v2(uintptr_t s, uintptr_t e,
+                                                              uint32_t init, bool inject,
+                                                              bool final, const lds_u32 *L,
+                                                              int lane) {
+  typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
+  const size_t len = e - s;
+  uint32_t x;
+  if (len < size_t(kCrcSmall)) {
+    uint32_t c = inject ? ~init : 0u;
+    if (lane == 0) {
+      gbl_u8 *p = (gbl_u8 *)s;
+      for (size_t i = 0; i < len; ++i) c = L[kV2ByteT0 + int((c ^ p[i]) & 0xffu)] ^ (c >> 8);
+    }
+    x = __builtin_amdgcn_readfirstlane(c);
+    return final ? ~x : x;
+  }
+  const uintptr_t A = s & ~uintptr_t(15), B = e & ~uintptr_t(15);
+  const uint32_t nb = uint32_t((B - A) >> 4);
+  const uint32_t K = (nb + 63u) >> 6;
+  const uintptr_t V = B - uintptr_t(K) * kLaneStride;
+  const uint32_t ninit = inject ? ~init : 0u;
+  const uint32_t lc = uint32_t(lane) & 31u;
+
+  uintptr_t blk = V + uintptr_t(lane) * 16u;
+  uint4 nxt = make_uint4(0, 0, 0, 0);
+  if (blk >= A) nxt = ldg16(blk);
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < K; ++k) {
+    uint4 w = nxt;
+    const uintptr_t cb = blk;
+    blk += kLaneStride;
+    if (k + 1 < K) nxt = ldg16(blk);  // software prefetch of the next 1 KiB
+    if (cb < A + 32u) {
+      w.x = head_fix(w.x, cb, s, ninit);
+      w.y = head_fix(w.y, cb + 4, s, ninit);
+      w.z = head_fix(w.z, cb + 8, s, ninit);
+      w.w = head_fix(w.w, cb + 12, s, ninit);
+    }
+    if (k) r = shift1008(L, r, lc);
+    r = step8(L, r ^ w.x, w.y, lc);
+    r = step8(L, r ^ w.z, w.w, lc);
+  }
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    uint32_t y = shift_tree(L, m, r);
+    y = __shfl_xor(y, 1 << m);
+    if (lane & (1 << m)) r ^= y;
+  }
+  const uint32_t t = uint32_t(e - B);
+  if (lane == 63 && t) {  // fold the <16-byte tail byte by byte (crc32c.c:131)
+    gbl_u8 *p = (gbl_u8 *)B;
+    for (uint32_t i = 0; i < t; ++i) r = L[kV2ByteT0 + int((r ^ p[i]) & 0xffu)] ^ (r >> 8);
+  }
+  x = __builtin_amdgcn_readlane(r, 63);
+  return final ? ~x : x;
+}
+
+template <int V>
+__device__ __forceinline__ uint32_t wave_crc_v(uintptr_t s, uintptr_t e, uint32_t init,
+                                               bool inject, bool final, const lds_u32 *L,
+                                               int lane) {
+  if constexpr (V == 2) return wave_crc_v2(s, e, init, inject, final, L, lane);
+  else return wave_crc(s, e, init, inject, final, L, lane);
+}
+
+template <int V> constexpr int crc_lds_words() { return V == 2 ? kCrcV2Words : kCrcTableWords; }
+
+extern __shared__ __attribute__((aligned(16))) uint32_t crc_lds[];
+
+__device__ __forceinline__ void load_tables(uint32_t *L, const uint32_t *g, int words) {
   const uint4 *src = reinterpret_cast<const uint4 *>(g);
   uint4 *dst = reinterpret_cast<uint4 *>(L);
-  for (int i = threadIdx.x; i < kCrcTableWords / 4; i += blockDim.x) dst[i] = src[i];
+  for (int i = threadIdx.x; i < words / 4; i += blockDim.x) dst[i] = src[i];
   __syncthreads();
 }
 
@@ -161,12 +276,13 @@ __device__ __forceinline__ uint32_t be32_at(const uint8_t *p) {
 }
 
 // ---- independent ranges ---------------------------------------------------
-__global__ __launch_bounds__(kCrcBlock) void crc32c_ranges_kernel(
+template <int V>
+__global__ __launch_bounds__(crc_block<V>()) void crc32c_ranges_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint32_t *__restrict__ lens, const uint32_t *__restrict__ init,
     uint32_t *__restrict__ out, uint32_t n, const uint32_t *__restrict__ gtab) {
-  __shared__ __attribute__((aligned(16))) uint32_t L[kCrcTableWords];
-  load_tables(L, gtab);
+  uint32_t *L = crc_lds;
+  load_tables(L, gtab, crc_lds_words<V>());
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wave = blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -174,17 +290,18 @@ __global__ __launch_bounds__(kCrcBlock) void crc32c_ranges_kernel(
   for (uint32_t i = wave; i < n; i += gridDim.x * wpb) {
     const uintptr_t s = reinterpret_cast<uintptr_t>(base) + offs[i];
     const uint32_t c0 = init ? init[i] : 0u;
-    const uint32_t crc = wave_crc(s, s + lens[i], c0, true, true, Lt, lane);
+    const uint32_t crc = wave_crc_v<V>(s, s + lens[i], c0, true, true, Lt, lane);
     if (lane == 0) out[i] = crc;
   }
 }
 
 // ---- one long range split into kCrcChunk chunks (raw registers) ------------
-__global__ __launch_bounds__(kCrcBlock) void crc32c_chunks_kernel(
+template <int V>
+__global__ __launch_bounds__(crc_block<V>()) void crc32c_chunks_kernel(
     const uint8_t *__restrict__ p, uint64_t len, uint32_t init, uint32_t *__restrict__ raw,
     uint32_t nchunks, const uint32_t *__restrict__ gtab) {
-  __shared__ __attribute__((aligned(16))) uint32_t L[kCrcTableWords];
-  load_tables(L, gtab);
+  uint32_t *L = crc_lds;
+  load_tables(L, gtab, crc_lds_words<V>());
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wave = blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -193,7 +310,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc32c_chunks_kernel(
     const uint64_t o = uint64_t(i) * kCrcChunk;
     const uint64_t l = (len - o < kCrcChunk) ? len - o : kCrcChunk;
     const uintptr_t s = reinterpret_cast<uintptr_t>(p) + o;
-    const uint32_t r = wave_crc(s, s + l, init, i == 0, false, Lt, lane);
+    const uint32_t r = wave_crc_v<V>(s, s + l, init, i == 0, false, Lt, lane);
     if (lane == 0) raw[i] = r;
   }
 }
@@ -232,13 +349,13 @@ __global__ void crc32c_combine_kernel(const uint32_t *__restrict__ raw, uint32_t
 }
 
 // ---- MsgVersion 2 record batches ------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(kCrcBlock) void crc32c_msgset_v2_kernel(
+template <int V, int MODE>
+__global__ __launch_bounds__(crc_block<V>()) void crc32c_msgset_v2_kernel(
     uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint32_t *__restrict__ caps, uint32_t *__restrict__ out, uint32_t n,
     const uint32_t *__restrict__ gtab) {
-  __shared__ __attribute__((aligned(16))) uint32_t L[kCrcTableWords];
-  load_tables(L, gtab);
+  uint32_t *L = crc_lds;
+  load_tables(L, gtab, crc_lds_words<V>());
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wave = blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -253,7 +370,7 @@ __global__ __launch_bounds__(kCrcBlock) void crc32c_msgset_v2_kernel(
     }
     const uintptr_t s = reinterpret_cast<uintptr_t>(hdr) + 21u;
     const uintptr_t e = reinterpret_cast<uintptr_t>(hdr) + 12u + length;
-    const uint32_t crc = wave_crc(s, e, 0u, true, true, Lt, lane);
+    const uint32_t crc = wave_crc_v<V>(s, e, 0u, true, true, Lt, lane);
     if (lane == 0) {
       if (MODE == RDK_HIP_V2_CRC_VERIFY) {
         out[i] = (be32_at(hdr + 17) == crc) ? 0u : 1u;
@@ -275,27 +392,43 @@ __global__ __launch_bounds__(kCrcBlock) void crc32c_msgset_v2_kernel(
 // ============================================================ host launchers
 namespace rdk {
 
-static unsigned crc_grid(uint32_t nwork) {
-  const uint32_t wpb = kCrcBlock / kWave;
+static int crc_variant() {
+  static const int v = (getenv("RDK_HIP_CRC_V1") && atoi(getenv("RDK_HIP_CRC_V1"))) ? 1 : 2;
+  return v;
+}
+
+template <int V> static unsigned crc_grid(uint32_t nwork) {
+  const uint32_t wpb = crc_block<V>() / kWave;
   uint32_t blocks = (nwork + wpb - 1) / wpb;
-  // 40 KiB LDS per workgroup -> 4 resident per CU; 256 CUs
-  if (blocks > 1024u) blocks = 1024u;
+  const uint32_t resident = V == 2 ? 2u * 256u : 4u * 256u;  // per-CU LDS residency x 256 CUs
+  if (blocks > resident) blocks = resident;
   return blocks ? blocks : 1u;
 }
 
-// CRC32C of one device buffer (any length) -> *d_result (device).  Used by the
-// drop-in crc32c()/rd_slice_crc32c() after the host gather + H2D copy.
+template <int V> static const uint32_t *tabs(int dev) {
+  return V == 2 ? crc_tables_v2_dev(dev) : crc_tables_dev(dev);
+}
+template <int V> static size_t lds_bytes() { return size_t(crc_lds_words<V>()) * 4u; }
+
+template <int V>
+static void launch_chunks(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
+                          uint32_t *d_scratch, uint32_t nchunks, hipStream_t s) {
+  hipLaunchKernelGGL(crc32c_chunks_kernel<V>, dim3(crc_grid<V>(nchunks)), dim3(crc_block<V>()),
+                     lds_bytes<V>(), s, d_buf, len, init, d_scratch, nchunks, tabs<V>(c->device));
+}
+
+// CRC32C of one device buffer (any length) -> d_scratch[nchunks] (device).
+// Used by the drop-in crc32c()/rd_slice_crc32c() after the host gather + H2D.
 int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
                       uint32_t *d_scratch /* >= nchunks+1 words */, hipStream_t s) {
   const uint32_t nchunks = len ? uint32_t((len + kCrcChunk - 1) / kCrcChunk) : 1u;
-  const uint32_t *tab = crc_tables_dev(c->device);
   if (len == 0) {
     // crc32c(crc, buf, 0) == crc: inversions cancel (crc32c.c:102,133)
     RDK_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_scratch + nchunks), init, 1, s));
     return 0;
   }
-  hipLaunchKernelGGL(crc32c_chunks_kernel, dim3(crc_grid(nchunks)), dim3(kCrcBlock), 0, s, d_buf,
-                     len, init, d_scratch, nchunks, tab);
+  if (crc_variant() == 2) launch_chunks<2>(c, d_buf, len, init, d_scratch, nchunks, s);
+  else launch_chunks<1>(c, d_buf, len, init, d_scratch, nchunks, s);
   hipLaunchKernelGGL(crc32c_combine_kernel, dim3(1), dim3(64), 0, s, d_scratch, nchunks, len,
                      d_scratch + nchunks, crc_x2n_dev(c->device));
   RDK_HIP_CHECK(hipGetLastError());
@@ -304,6 +437,30 @@ int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
 
 uint32_t crc_scratch_words(uint64_t len) {
   return (len ? uint32_t((len + kCrcChunk - 1) / kCrcChunk) : 1u) + 1u;
+}
+
+template <int V>
+static void launch_ranges(Ctx *c, const void *d_base, const uint64_t *d_offs,
+                          const uint32_t *d_lens, const uint32_t *d_init, uint32_t *d_out,
+                          uint32_t n, hipStream_t s) {
+  hipLaunchKernelGGL(crc32c_ranges_kernel<V>, dim3(crc_grid<V>(n)), dim3(crc_block<V>()),
+                     lds_bytes<V>(), s, static_cast<const uint8_t *>(d_base), d_offs, d_lens,
+                     d_init, d_out, n, tabs<V>(c->device));
+}
+
+template <int V, int MODE>
+static void launch_v2(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *caps,
+                      uint32_t *out, uint32_t n, hipStream_t s) {
+  hipLaunchKernelGGL((crc32c_msgset_v2_kernel<V, MODE>), dim3(crc_grid<V>(n)),
+                     dim3(crc_block<V>()), lds_bytes<V>(), s, b, offs, caps, out, n,
+                     tabs<V>(c->device));
+}
+
+template <int MODE>
+static void launch_v2_any(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *caps,
+                          uint32_t *out, uint32_t n, hipStream_t s) {
+  if (crc_variant() == 2) launch_v2<2, MODE>(c, b, offs, caps, out, n, s);
+  else launch_v2<1, MODE>(c, b, offs, caps, out, n, s);
 }
 
 }  // namespace rdk
@@ -318,9 +475,8 @@ RDK_API int rdk_hip_crc32c_ranges(const void *d_base, const uint64_t *d_offs,
   if (!n) return RDK_HIP_OK;
   if (!d_base || !d_offs || !d_lens || !d_out) return set_error(RDK_HIP_E_INVAL, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(crc32c_ranges_kernel, dim3(crc_grid(n)), dim3(kCrcBlock), 0, s,
-                     static_cast<const uint8_t *>(d_base), d_offs, d_lens, d_init, d_out, n,
-                     crc_tables_dev(c->device));
+  if (crc_variant() == 2) launch_ranges<2>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
+  else launch_ranges<1>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
   RDK_HIP_CHECK(hipGetLastError());
   return RDK_HIP_OK;
 }
@@ -335,20 +491,15 @@ RDK_API int rdk_hip_msgset_v2_crc(void *d_base, const uint64_t *d_batch_offs,
     return set_error(RDK_HIP_E_INVAL, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint8_t *b = static_cast<uint8_t *>(d_base);
-  const uint32_t *tab = crc_tables_dev(c->device);
-  const dim3 g(crc_grid(n)), blk(kCrcBlock);
   switch (mode) {
     case RDK_HIP_V2_CRC_COMPUTE:
-      hipLaunchKernelGGL(crc32c_msgset_v2_kernel<RDK_HIP_V2_CRC_COMPUTE>, g, blk, 0, s, b,
-                         d_batch_offs, d_batch_caps, d_out, n, tab);
+      launch_v2_any<RDK_HIP_V2_CRC_COMPUTE>(c, b, d_batch_offs, d_batch_caps, d_out, n, s);
       break;
     case RDK_HIP_V2_CRC_FINALIZE:
-      hipLaunchKernelGGL(crc32c_msgset_v2_kernel<RDK_HIP_V2_CRC_FINALIZE>, g, blk, 0, s, b,
-                         d_batch_offs, d_batch_caps, d_out, n, tab);
+      launch_v2_any<RDK_HIP_V2_CRC_FINALIZE>(c, b, d_batch_offs, d_batch_caps, d_out, n, s);
       break;
     case RDK_HIP_V2_CRC_VERIFY:
-      hipLaunchKernelGGL(crc32c_msgset_v2_kernel<RDK_HIP_V2_CRC_VERIFY>, g, blk, 0, s, b,
-                         d_batch_offs, d_batch_caps, d_out, n, tab);
+      launch_v2_any<RDK_HIP_V2_CRC_VERIFY>(c, b, d_batch_offs, d_batch_caps, d_out, n, s);
       break;
     default:
       return set_error(RDK_HIP_E_INVAL, "bad mode %d", mode);

@@ -58,6 +58,34 @@ void crc_build_tables(uint32_t *out) {
   }
 }
 
+void crc_build_tables_v2(uint32_t *out) {
+  static uint32_t T[kCrcTableWords];
+  crc_build_tables(T);  // byte slicing tables T[0..15]
+  // slicing-by-8 nibble tables (crc32c.c:97-134 sequence, split by nibble)
+  for (int k = 0; k < 8; ++k)
+    for (int hi = 0; hi < 2; ++hi)
+      for (uint32_t e = 0; e < 16; ++e) {
+        const uint32_t v = T[k * 256 + (e << (4 * hi))];
+        for (int c = 0; c < kNibCopies; ++c)
+          out[kNibSlice + (2 * k + hi) * kNibTable + e * kNibCopies + c] = v;
+      }
+  // advance the register over the 1008 zero bytes between a lane's vectors
+  uint32_t op[32];
+  crc_zeros_operator(op, size_t(kLaneStride - 16));
+  for (int j = 0; j < 8; ++j)
+    for (uint32_t e = 0; e < 16; ++e) {
+      const uint32_t v = crc_gf2_times(op, e << (4 * j));
+      for (int c = 0; c < kNibCopies; ++c) out[kNibShift + j * kNibTable + e * kNibCopies + c] = v;
+    }
+  for (uint32_t b = 0; b < 256; ++b) out[kV2ByteT0 + b] = T[b];
+  for (int m = 0; m < 6; ++m) {  // merge tree: advance by 16 << m bytes
+    crc_zeros_operator(op, size_t(16) << m);
+    for (int q = 0; q < 4; ++q)
+      for (uint32_t b = 0; b < 256; ++b)
+        out[kV2Tree + (m * 4 + q) * 256 + b] = crc_gf2_times(op, b << (8 * q));
+  }
+}
+
 // x2n[k] = x^(2^k) mod P in reflected form (bit 31 = x^0), for the
 // multiply-mod-P shift used when combining ranges of arbitrary length.
 static uint32_t multmodp(uint32_t a, uint32_t b) {

@@ -28,6 +28,22 @@ constexpr int kCrcTableWords = kCrcNumTables * 256;
 constexpr int crc_shift_table(int level) { return kCrcShiftBase + 4 * (level - 1); }
 
 void crc_build_tables(uint32_t *out /* kCrcTableWords */);
+
+// ---- v2 image (default): bank-conflict-free nibble tables -----------------
+// A byte lookup T[b] = N_lo[b & 15] ^ N_hi[b >> 4] (the tables are linear over
+// GF(2)).  Each 16-entry nibble table is stored 32 times, entry e of copy c at
+// dword e*32 + c, and lane l reads copy l%32: every lane of a 32-lane
+// ds_read_b32 group hits its own bank, so a lookup costs 2 LDS cycles instead
+// of the ~6.3 measured for random byte-table reads (profiles/).
+constexpr int kNibCopies = 32;
+constexpr int kNibTable = 16 * kNibCopies;           // dwords per nibble table
+constexpr int kNibSlice = 0;                          // 16 tables: T_k (k=0..7) lo/hi -> 2k+hi
+constexpr int kNibShift = 16 * kNibTable;             // 8 tables: shift-1008 of register nibble j
+constexpr int kV2ByteT0 = 24 * kNibTable;             // byte table T0 (tail / short ranges)
+constexpr int kV2Tree = kV2ByteT0 + 256;              // shift 16<<m, m=0..5: 4 byte tables each
+constexpr int kCrcV2Words = kV2Tree + 6 * 4 * 256;    // 18688 dwords = 73 KiB
+constexpr int kLaneStride = 1024;                     // bytes between a lane's vectors
+void crc_build_tables_v2(uint32_t *out /* kCrcV2Words */);
 void crc_build_x2n(uint32_t *out /* 64 */);
 
 // Host GF(2) helpers (also used by unit tests through the engine API).

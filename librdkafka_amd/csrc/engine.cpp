@@ -41,6 +41,7 @@ namespace {
 constexpr int kMaxDev = 64;
 std::mutex g_mu;
 uint32_t *g_tables[kMaxDev];
+uint32_t *g_tables_v2[kMaxDev];
 uint32_t *g_x2n[kMaxDev];
 
 int default_device() {
@@ -52,15 +53,20 @@ int upload_tables(int dev) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_tables[dev]) return 0;
   static uint32_t host_tab[kCrcTableWords];
+  static uint32_t host_tab2[kCrcV2Words];
   static uint32_t host_x2n[64];
   crc_build_tables(host_tab);
+  crc_build_tables_v2(host_tab2);
   crc_build_x2n(host_x2n);
-  uint32_t *d = nullptr, *x = nullptr;
+  uint32_t *d = nullptr, *d2 = nullptr, *x = nullptr;
   RDK_HIP_CHECK(hipMalloc(&d, sizeof host_tab));
+  RDK_HIP_CHECK(hipMalloc(&d2, sizeof host_tab2));
   RDK_HIP_CHECK(hipMalloc(&x, sizeof host_x2n));
   RDK_HIP_CHECK(hipMemcpy(d, host_tab, sizeof host_tab, hipMemcpyHostToDevice));
+  RDK_HIP_CHECK(hipMemcpy(d2, host_tab2, sizeof host_tab2, hipMemcpyHostToDevice));
   RDK_HIP_CHECK(hipMemcpy(x, host_x2n, sizeof host_x2n, hipMemcpyHostToDevice));
   g_tables[dev] = d;
+  g_tables_v2[dev] = d2;
   g_x2n[dev] = x;
   return 0;
 }
@@ -129,7 +135,8 @@ int ensure_host(Ctx *c, size_t bytes) {
 int ensure_dev(Ctx *c, int which, size_t bytes) {
   if (c->d_cap[which] >= bytes) return 0;
   if (c->d_stage[which]) {
-    (void)hipStreamSynchronize(c->stream);
+    // the buffer may be in flight on any stream the caller passed: drain all
+    (void)hipDeviceSynchronize();
     (void)hipFree(c->d_stage[which]);
   }
   c->d_stage[which] = nullptr;
@@ -142,7 +149,7 @@ int ensure_dev(Ctx *c, int which, size_t bytes) {
 int ensure_desc(Ctx *c, size_t bytes) {
   if (c->d_desc_cap >= bytes) return 0;
   if (c->d_desc) {
-    (void)hipStreamSynchronize(c->stream);
+    (void)hipDeviceSynchronize();
     (void)hipFree(c->d_desc);
     (void)hipHostFree(c->h_desc);
   }
@@ -154,6 +161,7 @@ int ensure_desc(Ctx *c, size_t bytes) {
 }
 
 const uint32_t *crc_tables_dev(int device) { return g_tables[device]; }
+const uint32_t *crc_tables_v2_dev(int device) { return g_tables_v2[device]; }
 const uint32_t *crc_x2n_dev(int device) { return g_x2n[device]; }
 
 }  // namespace rdk
@@ -166,5 +174,5 @@ RDK_API int rdk_hip_init(int device) {
 RDK_API const char *rdk_hip_last_error(void) { return rdk::last_error(); }
 
 RDK_API const char *rdk_hip_version(void) {
-  return "librdkafka_hip 0.1 gfx950 crc32c:wave-slice16-lds lz4c:wave-exact lz4d:wave-serial";
+  return "librdkafka_hip 0.1 gfx950 crc32c:wave-nibble32-lds lz4c:wave-exact lz4d:wave-serial";
 }

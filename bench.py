@@ -303,6 +303,26 @@ def leg_line(name, res, steps, world, cpu=None):
     return d
 
 
+# HBM bytes per launch from rocprofv3 PMC passes on this kernel and workload
+# (scripts/profile_crc.sh -> scripts/pmc_summary.py; FETCH_SIZE x2 on gfx950).
+# Counters cannot be read in-process, so the committed summary of the same
+# kernel build and batch shape is used; null when they do not match.
+CRC_PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_crc_v3", "summary.json")
+
+
+def pmc_traffic(path, alg_bytes):
+    if os.environ.get("RDK_HIP_CRC_V1"):
+        return None, None
+    try:
+        with open(path) as f:
+            s = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if int(s.get("alg_bytes_per_launch", -1)) != int(alg_bytes) or "traffic_bytes" not in s:
+        return None, None
+    return int(s["traffic_bytes"]), os.path.relpath(path, ROOT)
+
+
 # ------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
@@ -375,6 +395,10 @@ def main():
                          "alg_bytes_per_launch": res["alg_bytes"]},
             "cpu_baseline": None,
         }
+        traffic, src = pmc_traffic(CRC_PMC_SUMMARY, res["alg_bytes"])
+        if traffic is not None:
+            line["roofline"]["traffic"] = traffic
+            line["roofline"]["traffic_source"] = src
         if not args.no_cpu_baseline and world == 1:
             buf, n, size = res["host_sample"]
             line["cpu_baseline"] = cpu_baseline_crc(buf, n, size)

@@ -43,7 +43,7 @@ int ensure_desc(Ctx *c, size_t bytes);
 
 // Device-resident CRC tables for `device` (uploaded once per device).
 const uint32_t *crc_tables_dev(int device);     // v1: byte slicing-by-16 image
-const uint32_t *crc_tables_v2_dev(int device);  // v2: conflict-free nibble image
+const uint32_t *crc_tables_v3_dev(int device);  // v3: rotated-nibble image
 // x^(2^k) mod P table (k = 0..63) for arbitrary-length shifts.
 const uint32_t *crc_x2n_dev(int device);
 

@@ -8,11 +8,11 @@
 //   * one wavefront per byte range (a record batch), persistent grid;
 //   * lane l of iteration k owns the 16-byte vector at V + 1024k + 16l, so
 //     every global_load_dwordx4 of the wave reads 1 KiB contiguous (coalesced);
-//   * v2 (default): a lane advances its raw CRC register over the 1008-byte
-//     gap with an 8-lookup operator, then absorbs its 16 bytes with two
-//     slicing-by-8 steps (crc32c.c:110-125).  Every byte lookup is split into
-//     two nibble lookups in 32-fold replicated tables (one copy per LDS bank)
-//     so the random table reads are bank-conflict free;
+//   * v3 (default): a lane runs Horner over its 4-byte words, u = M(u ^ w),
+//     where M (advance 4 bytes; 1012 bytes for the first word of a vector,
+//     folding in the lane's 1008-byte gap) is evaluated as 8 lookups in
+//     32-fold replicated nibble tables: conflict-free LDS banks and one
+//     v_and_or_b32 per lookup address (crc32c_tables.h "v3 image");
 //   * v1 (RDK_HIP_CRC_V1=1): 16 byte slicing tables + 4-lookup 1024-byte
 //     operator; measured LDS-conflict bound (profiles/r01_crc_v1_*);
 //   * the 64 lane registers are merged by a 6-level xor-shuffle tree whose
@@ -30,9 +30,9 @@
 
 namespace rdk {
 
-// threads per workgroup: v2's 73 KiB of tables fit twice per CU -> 2 x 16 waves;
+// threads per workgroup: v3's 57 KiB of tables fit twice per CU -> 2 x 16 waves;
 // v1's 40 KiB fit four times -> 4 x 8 waves
-template <int V> constexpr int crc_block() { return V == 2 ? 1024 : 512; }
+template <int V> constexpr int crc_block() { return V == 3 ? 1024 : 512; }
 constexpr int kCrcSmall = 64;        // ranges shorter than this: serial lane
 constexpr uint32_t kCrcChunk = 65536; // split of long single ranges
 
@@ -159,46 +159,41 @@ __device__ __attribute__((always_inline)) uint32_t wave_crc(uintptr_t s, uintptr
 }
 
 
-// ---------------------------------------------------------------- v2 path
-__device__ __forceinline__ uint32_t nib(const lds_u32 *L, int table, uint32_t x, int sh,
-                                        uint32_t lc) {
-  // (nibble << 5) | lane%32: the two fields never overlap, so v_and_or_b32
-  return L[table + int((((x >> sh) & 15u) << 5) | lc)];
+// ---------------------------------------------------------------- v3 path
+// LDS read at absolute byte address `a` + immediate `off` (the dynamic LDS
+// block is the kernel's only LDS, so it starts at 0 -- checked on the host
+// side by the parity tests, any other base would fail every CRC).
+__device__ __forceinline__ uint32_t lds_rd(uint32_t a, uint32_t off) {
+  return *reinterpret_cast<const lds_u32 *>(size_t(a + off));
 }
 
-// slicing-by-8 on the 8 bytes (s, w): s bytes use T7..T4, w bytes T3..T0
-__device__ __forceinline__ uint32_t step8(const lds_u32 *L, uint32_t s, uint32_t w, uint32_t lc) {
-  uint32_t a = 0, b = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    a ^= nib(L, kNibSlice + (2 * (7 - q)) * kNibTable, s, 8 * q, lc) ^
-         nib(L, kNibSlice + (2 * (7 - q) + 1) * kNibTable, s, 8 * q + 4, lc);
-    b ^= nib(L, kNibSlice + (2 * (3 - q)) * kNibTable, w, 8 * q, lc) ^
-         nib(L, kNibSlice + (2 * (3 - q) + 1) * kNibTable, w, 8 * q + 4, lc);
-  }
-  return a ^ b;
+// M(x) ^ extra for map MAP (0: advance 1012 zero bytes, 1: advance 4), 8
+// lookups whose addresses are one v_and_or_b32 each (crc32c_tables.h "v3 image")
+template <int MAP>
+__device__ __forceinline__ uint32_t map_v3(uint32_t x, uint32_t lc4, uint32_t extra = 0u) {
+  const uint32_t y1 = __builtin_amdgcn_alignbit(x, x, 8);
+  const uint32_t y2 = __builtin_amdgcn_alignbit(x, x, 16);
+  const uint32_t y3 = __builtin_amdgcn_alignbit(x, x, 24);
+  constexpr uint32_t s7 = kV3S7 + MAP * 4 * 2048, s11 = kV3S11 + MAP * 4 * 128;
+  const uint32_t a0 = lds_rd((x & 0x780u) | lc4, s7), b0 = lds_rd((x & 0x7800u) | lc4, s11);
+  const uint32_t a1 = lds_rd((y1 & 0x780u) | lc4, s7 + 2048), b1 = lds_rd((y1 & 0x7800u) | lc4, s11 + 128);
+  const uint32_t a2 = lds_rd((y2 & 0x780u) | lc4, s7 + 4096), b2 = lds_rd((y2 & 0x7800u) | lc4, s11 + 256);
+  const uint32_t a3 = lds_rd((y3 & 0x780u) | lc4, s7 + 6144), b3 = lds_rd((y3 & 0x7800u) | lc4, s11 + 384);
+  return ((a0 ^ b0) ^ (a1 ^ b1)) ^ ((a2 ^ b2) ^ (a3 ^ b3)) ^ extra;
 }
 
-__device__ __forceinline__ uint32_t shift1008(const lds_u32 *L, uint32_t x, uint32_t lc) {
-  uint32_t a = 0, b = 0;
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    a ^= nib(L, kNibShift + j * kNibTable, x, 4 * j, lc);
-    b ^= nib(L, kNibShift + (j + 1) * kNibTable, x, 4 * j + 4, lc);
-  }
-  return a ^ b;
+__device__ __forceinline__ uint32_t byte_tab(int i, uint32_t b) {
+  return lds_rd(b << 2, uint32_t(v3_byte_table(i)));
 }
 
-__device__ __forceinline__ uint32_t shift_tree(const lds_u32 *L, int m, uint32_t x) {
-  const int t = kV2Tree + m * 1024;
-  return L[t + int(x & 0xffu)] ^ L[t + 256 + int((x >> 8) & 0xffu)] ^
-         L[t + 512 + int((x >> 16) & 0xffu)] ^ L[t + 768 + int(x >> 24)];
+__device__ __forceinline__ uint32_t shift_tree_v3(int m, uint32_t x) {
+  return byte_tab(m * 4, x & 0xffu) ^ byte_tab(m * 4 + 1, (x >> 8) & 0xffu) ^
+         byte_tab(m * 4 + 2, (x >> 16) & 0xffu) ^ byte_tab(m * 4 + 3, x >> 24);
 }
 
-__device__ __attribute__((always_inline)) uint32_t wave_crc_v2(uintptr_t s, uintptr_t e,
+__device__ __attribute__((always_inline)) uint32_t wave_crc_v3(uintptr_t s, uintptr_t e,
                                                               uint32_t init, bool inject,
-                                                              bool final, const lds_u32 *L,
-                                                              int lane) {
+                                                              bool final, int lane) {
   typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
   const size_t len = e - s;
   uint32_t x;
@@ -206,7 +201,7 @@ __device__ __attribute__((always_inline)) uint32_t wave_crc_v2(uintptr_t s, uint
     uint32_t c = inject ? ~init : 0u;
     if (lane == 0) {
       gbl_u8 *p = (gbl_u8 *)s;
-      for (size_t i = 0; i < len; ++i) c = L[kV2ByteT0 + int((c ^ p[i]) & 0xffu)] ^ (c >> 8);
+      for (size_t i = 0; i < len; ++i) c = byte_tab(kV3T0, (c ^ p[i]) & 0xffu) ^ (c >> 8);
     }
     x = __builtin_amdgcn_readfirstlane(c);
     return final ? ~x : x;
@@ -216,12 +211,12 @@ __device__ __attribute__((always_inline)) uint32_t wave_crc_v2(uintptr_t s, uint
   const uint32_t K = (nb + 63u) >> 6;
   const uintptr_t V = B - uintptr_t(K) * kLaneStride;
   const uint32_t ninit = inject ? ~init : 0u;
-  const uint32_t lc = uint32_t(lane) & 31u;
+  const uint32_t lc4 = (uint32_t(lane) & 31u) << 2;
 
   uintptr_t blk = V + uintptr_t(lane) * 16u;
   uint4 nxt = make_uint4(0, 0, 0, 0);
   if (blk >= A) nxt = ldg16(blk);
-  uint32_t r = 0;
+  uint32_t u = 0;
   for (uint32_t k = 0; k < K; ++k) {
     uint4 w = nxt;
     const uintptr_t cb = blk;
@@ -233,20 +228,24 @@ __device__ __attribute__((always_inline)) uint32_t wave_crc_v2(uintptr_t s, uint
       w.z = head_fix(w.z, cb + 8, s, ninit);
       w.w = head_fix(w.w, cb + 12, s, ninit);
     }
-    if (k) r = shift1008(L, r, lc);
-    r = step8(L, r ^ w.x, w.y, lc);
-    r = step8(L, r ^ w.z, w.w, lc);
+    // Horner over 4-byte words (slicing-by-4 per word, crc32c.c:110-125);
+    // the lane's 1008-byte gap is folded into the first word's map
+    u = k ? map_v3<0>(u, lc4, w.x) : w.x;
+    u = map_v3<1>(u, lc4, w.y);
+    u = map_v3<1>(u, lc4, w.z);
+    u = map_v3<1>(u, lc4, w.w);
   }
+  uint32_t r = map_v3<1>(u, lc4);
 #pragma unroll
   for (int m = 0; m < 6; ++m) {
-    uint32_t y = shift_tree(L, m, r);
+    uint32_t y = shift_tree_v3(m, r);
     y = __shfl_xor(y, 1 << m);
     if (lane & (1 << m)) r ^= y;
   }
   const uint32_t t = uint32_t(e - B);
   if (lane == 63 && t) {  // fold the <16-byte tail byte by byte (crc32c.c:131)
     gbl_u8 *p = (gbl_u8 *)B;
-    for (uint32_t i = 0; i < t; ++i) r = L[kV2ByteT0 + int((r ^ p[i]) & 0xffu)] ^ (r >> 8);
+    for (uint32_t i = 0; i < t; ++i) r = byte_tab(kV3T0, (r ^ p[i]) & 0xffu) ^ (r >> 8);
   }
   x = __builtin_amdgcn_readlane(r, 63);
   return final ? ~x : x;
@@ -256,11 +255,11 @@ template <int V>
 __device__ __forceinline__ uint32_t wave_crc_v(uintptr_t s, uintptr_t e, uint32_t init,
                                                bool inject, bool final, const lds_u32 *L,
                                                int lane) {
-  if constexpr (V == 2) return wave_crc_v2(s, e, init, inject, final, L, lane);
+  if constexpr (V == 3) return wave_crc_v3(s, e, init, inject, final, lane);
   else return wave_crc(s, e, init, inject, final, L, lane);
 }
 
-template <int V> constexpr int crc_lds_words() { return V == 2 ? kCrcV2Words : kCrcTableWords; }
+template <int V> constexpr int crc_lds_words() { return V == 3 ? kCrcV3Words : kCrcTableWords; }
 
 extern __shared__ __attribute__((aligned(16))) uint32_t crc_lds[];
 
@@ -393,20 +392,20 @@ __global__ __launch_bounds__(crc_block<V>()) void crc32c_msgset_v2_kernel(
 namespace rdk {
 
 static int crc_variant() {
-  static const int v = (getenv("RDK_HIP_CRC_V1") && atoi(getenv("RDK_HIP_CRC_V1"))) ? 1 : 2;
+  static const int v = (getenv("RDK_HIP_CRC_V1") && atoi(getenv("RDK_HIP_CRC_V1"))) ? 1 : 3;
   return v;
 }
 
 template <int V> static unsigned crc_grid(uint32_t nwork) {
   const uint32_t wpb = crc_block<V>() / kWave;
   uint32_t blocks = (nwork + wpb - 1) / wpb;
-  const uint32_t resident = V == 2 ? 2u * 256u : 4u * 256u;  // per-CU LDS residency x 256 CUs
+  const uint32_t resident = V == 3 ? 2u * 256u : 4u * 256u;  // per-CU LDS residency x 256 CUs
   if (blocks > resident) blocks = resident;
   return blocks ? blocks : 1u;
 }
 
 template <int V> static const uint32_t *tabs(int dev) {
-  return V == 2 ? crc_tables_v2_dev(dev) : crc_tables_dev(dev);
+  return V == 3 ? crc_tables_v3_dev(dev) : crc_tables_dev(dev);
 }
 template <int V> static size_t lds_bytes() { return size_t(crc_lds_words<V>()) * 4u; }
 
@@ -427,7 +426,7 @@ int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
     RDK_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_scratch + nchunks), init, 1, s));
     return 0;
   }
-  if (crc_variant() == 2) launch_chunks<2>(c, d_buf, len, init, d_scratch, nchunks, s);
+  if (crc_variant() == 3) launch_chunks<3>(c, d_buf, len, init, d_scratch, nchunks, s);
   else launch_chunks<1>(c, d_buf, len, init, d_scratch, nchunks, s);
   hipLaunchKernelGGL(crc32c_combine_kernel, dim3(1), dim3(64), 0, s, d_scratch, nchunks, len,
                      d_scratch + nchunks, crc_x2n_dev(c->device));
@@ -459,7 +458,7 @@ static void launch_v2(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *
 template <int MODE>
 static void launch_v2_any(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *caps,
                           uint32_t *out, uint32_t n, hipStream_t s) {
-  if (crc_variant() == 2) launch_v2<2, MODE>(c, b, offs, caps, out, n, s);
+  if (crc_variant() == 3) launch_v2<3, MODE>(c, b, offs, caps, out, n, s);
   else launch_v2<1, MODE>(c, b, offs, caps, out, n, s);
 }
 
@@ -475,7 +474,7 @@ RDK_API int rdk_hip_crc32c_ranges(const void *d_base, const uint64_t *d_offs,
   if (!n) return RDK_HIP_OK;
   if (!d_base || !d_offs || !d_lens || !d_out) return set_error(RDK_HIP_E_INVAL, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (crc_variant() == 2) launch_ranges<2>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
+  if (crc_variant() == 3) launch_ranges<3>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
   else launch_ranges<1>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
   RDK_HIP_CHECK(hipGetLastError());
   return RDK_HIP_OK;

@@ -58,31 +58,35 @@ void crc_build_tables(uint32_t *out) {
   }
 }
 
-void crc_build_tables_v2(uint32_t *out) {
-  static uint32_t T[kCrcTableWords];
-  crc_build_tables(T);  // byte slicing tables T[0..15]
-  // slicing-by-8 nibble tables (crc32c.c:97-134 sequence, split by nibble)
-  for (int k = 0; k < 8; ++k)
-    for (int hi = 0; hi < 2; ++hi)
-      for (uint32_t e = 0; e < 16; ++e) {
-        const uint32_t v = T[k * 256 + (e << (4 * hi))];
-        for (int c = 0; c < kNibCopies; ++c)
-          out[kNibSlice + (2 * k + hi) * kNibTable + e * kNibCopies + c] = v;
-      }
-  // advance the register over the 1008 zero bytes between a lane's vectors
+void crc_build_tables_v3(uint32_t *out) {
+  std::memset(out, 0, size_t(kCrcV3Bytes));
   uint32_t op[32];
-  crc_zeros_operator(op, size_t(kLaneStride - 16));
-  for (int j = 0; j < 8; ++j)
-    for (uint32_t e = 0; e < 16; ++e) {
-      const uint32_t v = crc_gf2_times(op, e << (4 * j));
-      for (int c = 0; c < kNibCopies; ++c) out[kNibShift + j * kNibTable + e * kNibCopies + c] = v;
-    }
-  for (uint32_t b = 0; b < 256; ++b) out[kV2ByteT0 + b] = T[b];
+  for (int map = 0; map < 2; ++map) {
+    crc_zeros_operator(op, map == 0 ? size_t(kLaneStride - 12) : size_t(4));
+    for (int j = 0; j < 4; ++j)      // rotation y_j = rotr(x, 8j)
+      for (int h = 0; h < 2; ++h)    // group at bits 7+4h .. 10+4h of y_j
+        for (uint32_t e = 0; e < 16; ++e) {
+          const uint32_t y = e << (7 + 4 * h);
+          const uint32_t x = (j == 0) ? y : ((y << (8 * j)) | (y >> (32 - 8 * j)));
+          const uint32_t v = crc_gf2_times(op, x);
+          const int t = map * 4 + j;
+          for (int c = 0; c < 32; ++c) {
+            const int byte = h == 0 ? kV3S7 + t * 2048 + int(e) * 128 + c * 4
+                                    : kV3S11 + t * 128 + int(e) * 2048 + c * 4;
+            out[byte / 4] = v;
+          }
+        }
+  }
   for (int m = 0; m < 6; ++m) {  // merge tree: advance by 16 << m bytes
     crc_zeros_operator(op, size_t(16) << m);
     for (int q = 0; q < 4; ++q)
       for (uint32_t b = 0; b < 256; ++b)
-        out[kV2Tree + (m * 4 + q) * 256 + b] = crc_gf2_times(op, b << (8 * q));
+        out[v3_byte_table(m * 4 + q) / 4 + int(b)] = crc_gf2_times(op, b << (8 * q));
+  }
+  for (uint32_t b = 0; b < 256; ++b) {  // T0 (crc32c.c:69-78)
+    uint32_t r = b;
+    for (int i = 0; i < 8; ++i) r = (r >> 1) ^ ((r & 1u) ? kCrcPoly : 0u);
+    out[v3_byte_table(kV3T0) / 4 + int(b)] = r;
   }
 }
 

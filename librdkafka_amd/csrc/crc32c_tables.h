@@ -29,21 +29,31 @@ constexpr int crc_shift_table(int level) { return kCrcShiftBase + 4 * (level - 1
 
 void crc_build_tables(uint32_t *out /* kCrcTableWords */);
 
-// ---- v2 image (default): bank-conflict-free nibble tables -----------------
-// A byte lookup T[b] = N_lo[b & 15] ^ N_hi[b >> 4] (the tables are linear over
-// GF(2)).  Each 16-entry nibble table is stored 32 times, entry e of copy c at
-// dword e*32 + c, and lane l reads copy l%32: every lane of a 32-lane
-// ds_read_b32 group hits its own bank, so a lookup costs 2 LDS cycles instead
-// of the ~6.3 measured for random byte-table reads (profiles/).
-constexpr int kNibCopies = 32;
-constexpr int kNibTable = 16 * kNibCopies;           // dwords per nibble table
-constexpr int kNibSlice = 0;                          // 16 tables: T_k (k=0..7) lo/hi -> 2k+hi
-constexpr int kNibShift = 16 * kNibTable;             // 8 tables: shift-1008 of register nibble j
-constexpr int kV2ByteT0 = 24 * kNibTable;             // byte table T0 (tail / short ranges)
-constexpr int kV2Tree = kV2ByteT0 + 256;              // shift 16<<m, m=0..5: 4 byte tables each
-constexpr int kCrcV2Words = kV2Tree + 6 * 4 * 256;    // 18688 dwords = 73 KiB
-constexpr int kLaneStride = 1024;                     // bytes between a lane's vectors
-void crc_build_tables_v2(uint32_t *out /* kCrcV2Words */);
+// ---- v3 image (default): rotated-nibble tables, conflict-free and 1-VALU addresses
+// A 32->32 GF(2)-linear map F (the CRC register advanced over n zero bytes) is
+// evaluated as the xor of 8 lookups, one per 4-bit group of its input x.  The
+// groups are bits [7..10] and [11..14] of y_j = rotr(x, 8j), j = 0..3, so each
+// lookup address is a single v_and_or_b32: (y_j & 0x780 | lc4) for "S7" tables
+// (16 entries x 32 copies, entry stride 128 B) or (y_j & 0x7800 | lc4) for
+// "S11" tables (entry stride 2 KiB; 16 of them interleave in one 32 KiB region,
+// table slot at bits 7..10 comes from the ds_read immediate offset).  lc4 =
+// 4*(lane%32): each 32-lane ds_read_b32 group hits 32 distinct banks.
+// Two maps are stored: M_1012 (map 0: the 1008-byte lane gap + one word) and
+// M_4 (map 1: one 4-byte word), which is all a lane's Horner update needs:
+//   u = M_1012(u) ^ w.x; u = M_4(u) ^ w.y; u = M_4(u) ^ w.z; u = M_4(u) ^ w.w.
+// The unused slots 8..15 of the S11 region (1 KiB contiguous per entry row)
+// hold 16 of the 25 byte tables (6x4 merge-tree operators + T0).
+constexpr int kV3S11 = 0;                       // bytes; slot t at +128*t, entry e at +2048*e
+constexpr int kV3S7 = 32768;                    // bytes; table t at +2048*t, entry e at +128*e
+constexpr int kV3ByteHi = 49152;                // byte tables 16..24
+constexpr int kV3NumByteTables = 25;            // tree (m*4+q, m=0..5), T0 = 24
+constexpr int kV3T0 = 24;
+constexpr int kCrcV3Bytes = kV3ByteHi + 9 * 1024;  // 58368 B = 57 KiB
+constexpr int kCrcV3Words = kCrcV3Bytes / 4;
+constexpr int kLaneStride = 1024;               // bytes between a lane's vectors
+// byte offset of byte table i (256 dwords, contiguous)
+constexpr int v3_byte_table(int i) { return i < 16 ? i * 2048 + 1024 : kV3ByteHi + (i - 16) * 1024; }
+void crc_build_tables_v3(uint32_t *out /* kCrcV3Words */);
 void crc_build_x2n(uint32_t *out /* 64 */);
 
 // Host GF(2) helpers (also used by unit tests through the engine API).

@@ -41,7 +41,7 @@ namespace {
 constexpr int kMaxDev = 64;
 std::mutex g_mu;
 uint32_t *g_tables[kMaxDev];
-uint32_t *g_tables_v2[kMaxDev];
+uint32_t *g_tables_v3[kMaxDev];
 uint32_t *g_x2n[kMaxDev];
 
 int default_device() {
@@ -53,10 +53,10 @@ int upload_tables(int dev) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_tables[dev]) return 0;
   static uint32_t host_tab[kCrcTableWords];
-  static uint32_t host_tab2[kCrcV2Words];
+  static uint32_t host_tab2[kCrcV3Words];
   static uint32_t host_x2n[64];
   crc_build_tables(host_tab);
-  crc_build_tables_v2(host_tab2);
+  crc_build_tables_v3(host_tab2);
   crc_build_x2n(host_x2n);
   uint32_t *d = nullptr, *d2 = nullptr, *x = nullptr;
   RDK_HIP_CHECK(hipMalloc(&d, sizeof host_tab));
@@ -66,7 +66,7 @@ int upload_tables(int dev) {
   RDK_HIP_CHECK(hipMemcpy(d2, host_tab2, sizeof host_tab2, hipMemcpyHostToDevice));
   RDK_HIP_CHECK(hipMemcpy(x, host_x2n, sizeof host_x2n, hipMemcpyHostToDevice));
   g_tables[dev] = d;
-  g_tables_v2[dev] = d2;
+  g_tables_v3[dev] = d2;
   g_x2n[dev] = x;
   return 0;
 }
@@ -161,7 +161,7 @@ int ensure_desc(Ctx *c, size_t bytes) {
 }
 
 const uint32_t *crc_tables_dev(int device) { return g_tables[device]; }
-const uint32_t *crc_tables_v2_dev(int device) { return g_tables_v2[device]; }
+const uint32_t *crc_tables_v3_dev(int device) { return g_tables_v3[device]; }
 const uint32_t *crc_x2n_dev(int device) { return g_x2n[device]; }
 
 }  // namespace rdk
@@ -174,5 +174,5 @@ RDK_API int rdk_hip_init(int device) {
 RDK_API const char *rdk_hip_last_error(void) { return rdk::last_error(); }
 
 RDK_API const char *rdk_hip_version(void) {
-  return "librdkafka_hip 0.1 gfx950 crc32c:wave-nibble32-lds lz4c:wave-exact lz4d:wave-serial";
+  return "librdkafka_hip 0.1 gfx950 crc32c:wave-rotnib-lds lz4c:wave-exact lz4d:wave-serial";
 }

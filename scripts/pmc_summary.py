@@ -1,0 +1,85 @@
+"""Summarise a rocprofv3 profile directory into profiles/<name>/summary.json.
+
+Layout expected (as written by scripts/profile_*.sh):
+  <dir>/trace/*_kernel_trace.csv          (--kernel-trace)
+  <dir>/pmc_fetch/*_counter_collection.csv (--pmc FETCH_SIZE)
+  <dir>/pmc_write/*_counter_collection.csv (--pmc WRITE_SIZE)
+  <dir>/pmc_sq/*_counter_collection.csv    (--pmc SQ_* group, optional)
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
+(16 B/lane) streaming read, so it is doubled.  bench.py reads `traffic_bytes`
+from the summary of the kernel and workload it measures.
+
+usage: python scripts/pmc_summary.py DIR KERNEL_SUBSTR ALG_BYTES_PER_LAUNCH OUT.json [--grid N]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def _rows(path_glob):
+    out = []
+    for p in sorted(glob.glob(path_glob)):
+        with open(p, newline="") as f:
+            out.extend(csv.DictReader(f))
+    return out
+
+
+def _match(row, kernel, grid):
+    if kernel not in row["Kernel_Name"]:
+        return False
+    g = row.get("Grid_Size", row.get("Grid_Size_X"))
+    return grid is None or int(g) == grid
+
+
+def counters(d, kernel, grid):
+    vals = {}
+    for r in _rows(os.path.join(d, "*_counter_collection.csv")):
+        if _match(r, kernel, grid):
+            vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}, max((len(v) for v in vals.values()), default=0)
+
+
+def summarise(d, kernel, alg_bytes, grid=None):
+    trace = [r for r in _rows(os.path.join(d, "trace", "*_kernel_trace.csv")) if _match(r, kernel, grid)]
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace]
+    s = {"kernel": kernel, "grid": grid, "launches_traced": len(durs),
+         "avg_ns": sum(durs) / len(durs) if durs else None,
+         "min_ns": min(durs) if durs else None,
+         "alg_bytes_per_launch": alg_bytes}
+    fetch, _ = counters(os.path.join(d, "pmc_fetch"), kernel, grid)
+    write, _ = counters(os.path.join(d, "pmc_write"), kernel, grid)
+    sq, _ = counters(os.path.join(d, "pmc_sq"), kernel, grid)
+    if "FETCH_SIZE" in fetch and "WRITE_SIZE" in write:
+        fb = fetch["FETCH_SIZE"] * 1024.0 * 2.0  # gfx950: FETCH_SIZE = 1/2 of streamed bytes
+        wb = write["WRITE_SIZE"] * 1024.0
+        s.update(fetch_bytes=fb, write_bytes=wb, traffic_bytes=fb + wb,
+                 traffic_over_alg=(fb + wb) / alg_bytes if alg_bytes else None,
+                 counter_note="FETCH_SIZE KiB x1024 x2 (gfx950 correction) + WRITE_SIZE KiB x1024")
+    if s["avg_ns"]:
+        s["achieved_GBps_alg"] = alg_bytes / s["avg_ns"]
+    if sq:
+        s["sq"] = sq
+        if sq.get("SQ_LDS_IDX_ACTIVE"):
+            s["lds_bank_conflict_frac"] = sq.get("SQ_LDS_BANK_CONFLICT", 0.0) / sq["SQ_LDS_IDX_ACTIVE"]
+    return s
+
+
+def main(argv):
+    grid = None
+    if "--grid" in argv:
+        i = argv.index("--grid")
+        grid = int(argv[i + 1])
+        argv = argv[:i] + argv[i + 2:]
+    d, kernel, alg, out = argv[1], argv[2], float(argv[3]), argv[4]
+    s = summarise(d, kernel, alg, grid)
+    with open(out, "w") as f:
+        json.dump(s, f, indent=1, sort_keys=True)
+    print(json.dumps(s, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main(sys.argv)

@@ -167,6 +167,14 @@ __device__ __forceinline__ uint32_t lds_rd(uint32_t a, uint32_t off) {
   return *reinterpret_cast<const lds_u32 *>(size_t(a + off));
 }
 
+// a ^ b ^ c in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96 (the
+// compiler emits two v_xor_b32 for it)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
 // M(x) ^ extra for map MAP (0: advance 1012 zero bytes, 1: advance 4), 8
 // lookups whose addresses are one v_and_or_b32 each (crc32c_tables.h "v3 image")
 template <int MAP>
@@ -179,7 +187,7 @@ __device__ __forceinline__ uint32_t map_v3(uint32_t x, uint32_t lc4, uint32_t ex
   const uint32_t a1 = lds_rd((y1 & 0x780u) | lc4, s7 + 2048), b1 = lds_rd((y1 & 0x7800u) | lc4, s11 + 128);
   const uint32_t a2 = lds_rd((y2 & 0x780u) | lc4, s7 + 4096), b2 = lds_rd((y2 & 0x7800u) | lc4, s11 + 256);
   const uint32_t a3 = lds_rd((y3 & 0x780u) | lc4, s7 + 6144), b3 = lds_rd((y3 & 0x7800u) | lc4, s11 + 384);
-  return ((a0 ^ b0) ^ (a1 ^ b1)) ^ ((a2 ^ b2) ^ (a3 ^ b3)) ^ extra;
+  return xor3(xor3(a0, b0, a1), xor3(b1, a2, b2), xor3(a3, b3, extra));
 }
 
 __device__ __forceinline__ uint32_t byte_tab(int i, uint32_t b) {
@@ -189,6 +197,44 @@ __device__ __forceinline__ uint32_t byte_tab(int i, uint32_t b) {
 __device__ __forceinline__ uint32_t shift_tree_v3(int m, uint32_t x) {
   return byte_tab(m * 4, x & 0xffu) ^ byte_tab(m * 4 + 1, (x >> 8) & 0xffu) ^
          byte_tab(m * 4 + 2, (x >> 16) & 0xffu) ^ byte_tab(m * 4 + 3, x >> 24);
+}
+
+// Absorb one lane's 16-byte vector (at cb) into its register: Horner over
+// 4-byte words (the slicing-by-4 step of crc32c.c:110-125), with the 1008
+// bytes owned by the other lanes folded into the first word's map.
+template <bool HEAD>
+__device__ __forceinline__ void absorb_vec(uint32_t &u, uint4 w, uintptr_t cb, uintptr_t A,
+                                           uintptr_t s, uint32_t ninit, uint32_t lc4,
+                                           bool first) {
+  if (HEAD && cb < A + 32u) {  // head: zero bytes before s, inject the running crc
+    w.x = head_fix(w.x, cb, s, ninit);
+    w.y = head_fix(w.y, cb + 4, s, ninit);
+    w.z = head_fix(w.z, cb + 8, s, ninit);
+    w.w = head_fix(w.w, cb + 12, s, ninit);
+  }
+  u = first ? w.x : map_v3<0>(u, lc4, w.x);
+  u = map_v3<1>(u, lc4, w.y);
+  u = map_v3<1>(u, lc4, w.z);
+  u = map_v3<1>(u, lc4, w.w);
+}
+
+constexpr int kCrcPrefetch = 4;  // 1 KiB wave steps in flight per wave
+
+// steps k0 .. k0+kCrcPrefetch-1; buffer j is reloaded right after use (3 KiB
+// per wave stay in flight while it is absorbed)
+template <bool HEAD>
+__device__ __forceinline__ void crc_round(uint32_t &u, uint4 (&buf)[kCrcPrefetch], uint32_t k0,
+                                          uint32_t K, uintptr_t base, uintptr_t A, uintptr_t s,
+                                          uint32_t ninit, uint32_t lc4) {
+#pragma unroll
+  for (int j = 0; j < kCrcPrefetch; ++j) {
+    const uint32_t k = k0 + uint32_t(j);
+    if (k < K) {
+      const uintptr_t cb = base + uintptr_t(k) * kLaneStride;
+      absorb_vec<HEAD>(u, buf[j], cb, A, s, ninit, lc4, HEAD && j == 0);
+      if (k + kCrcPrefetch < K) buf[j] = ldg16(cb + kCrcPrefetch * kLaneStride);
+    }
+  }
 }
 
 __device__ __attribute__((always_inline)) uint32_t wave_crc_v3(uintptr_t s, uintptr_t e,
@@ -208,33 +254,27 @@ __device__ __attribute__((always_inline)) uint32_t wave_crc_v3(uintptr_t s, uint
   }
   const uintptr_t A = s & ~uintptr_t(15), B = e & ~uintptr_t(15);
   const uint32_t nb = uint32_t((B - A) >> 4);
-  const uint32_t K = (nb + 63u) >> 6;
+  const uint32_t K = (nb + 63u) >> 6;  // 1 KiB wave steps
   const uintptr_t V = B - uintptr_t(K) * kLaneStride;
   const uint32_t ninit = inject ? ~init : 0u;
   const uint32_t lc4 = (uint32_t(lane) & 31u) << 2;
 
-  uintptr_t blk = V + uintptr_t(lane) * 16u;
-  uint4 nxt = make_uint4(0, 0, 0, 0);
-  if (blk >= A) nxt = ldg16(blk);
-  uint32_t u = 0;
-  for (uint32_t k = 0; k < K; ++k) {
-    uint4 w = nxt;
-    const uintptr_t cb = blk;
-    blk += kLaneStride;
-    if (k + 1 < K) nxt = ldg16(blk);  // software prefetch of the next 1 KiB
-    if (cb < A + 32u) {
-      w.x = head_fix(w.x, cb, s, ninit);
-      w.y = head_fix(w.y, cb + 4, s, ninit);
-      w.z = head_fix(w.z, cb + 8, s, ninit);
-      w.w = head_fix(w.w, cb + 12, s, ninit);
-    }
-    // Horner over 4-byte words (slicing-by-4 per word, crc32c.c:110-125);
-    // the lane's 1008-byte gap is folded into the first word's map
-    u = k ? map_v3<0>(u, lc4, w.x) : w.x;
-    u = map_v3<1>(u, lc4, w.y);
-    u = map_v3<1>(u, lc4, w.z);
-    u = map_v3<1>(u, lc4, w.w);
+  // kCrcPrefetch register buffers rotate through the steps: buffer j holds
+  // step k0+j and is reloaded with step k0+j+kCrcPrefetch as soon as it has
+  // been absorbed (no register copies; up to 4 KiB per wave in flight).
+  // Only step 0 can start below A, and the head ([s, s+4)) lies in steps 0-1.
+  const uintptr_t base = V + uintptr_t(lane) * 16u;
+  uint4 buf[kCrcPrefetch];
+#pragma unroll
+  for (int j = 0; j < kCrcPrefetch; ++j) {
+    buf[j] = make_uint4(0, 0, 0, 0);
+    const uintptr_t a = base + uintptr_t(j) * kLaneStride;
+    if (uint32_t(j) < K && a >= A) buf[j] = ldg16(a);
   }
+  uint32_t u = 0;
+  crc_round<true>(u, buf, 0u, K, base, A, s, ninit, lc4);  // steps 0-3 (head)
+  for (uint32_t k0 = kCrcPrefetch; k0 < K; k0 += kCrcPrefetch)
+    crc_round<false>(u, buf, k0, K, base, A, s, ninit, lc4);
   uint32_t r = map_v3<1>(u, lc4);
 #pragma unroll
   for (int m = 0; m < 6; ++m) {
@@ -276,7 +316,7 @@ __device__ __forceinline__ uint32_t be32_at(const uint8_t *p) {
 
 // ---- independent ranges ---------------------------------------------------
 template <int V>
-__global__ __launch_bounds__(crc_block<V>()) void crc32c_ranges_kernel(
+__global__ __launch_bounds__(crc_block<V>(), 8) void crc32c_ranges_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint32_t *__restrict__ lens, const uint32_t *__restrict__ init,
     uint32_t *__restrict__ out, uint32_t n, const uint32_t *__restrict__ gtab) {
@@ -296,7 +336,7 @@ __global__ __launch_bounds__(crc_block<V>()) void crc32c_ranges_kernel(
 
 // ---- one long range split into kCrcChunk chunks (raw registers) ------------
 template <int V>
-__global__ __launch_bounds__(crc_block<V>()) void crc32c_chunks_kernel(
+__global__ __launch_bounds__(crc_block<V>(), 8) void crc32c_chunks_kernel(
     const uint8_t *__restrict__ p, uint64_t len, uint32_t init, uint32_t *__restrict__ raw,
     uint32_t nchunks, const uint32_t *__restrict__ gtab) {
   uint32_t *L = crc_lds;
@@ -349,7 +389,7 @@ __global__ void crc32c_combine_kernel(const uint32_t *__restrict__ raw, uint32_t
 
 // ---- MsgVersion 2 record batches ------------------------------------------
 template <int V, int MODE>
-__global__ __launch_bounds__(crc_block<V>()) void crc32c_msgset_v2_kernel(
+__global__ __launch_bounds__(crc_block<V>(), 8) void crc32c_msgset_v2_kernel(
     uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint32_t *__restrict__ caps, uint32_t *__restrict__ out, uint32_t n,
     const uint32_t *__restrict__ gtab) {

@@ -70,7 +70,10 @@ __device__ __forceinline__ uint32_t win_byte(InWin &w, uintptr_t p, int lane) {
     w.nxt = ld_dw(w.base + 256u + 4u * lane, w.lim);
   }
   const uint32_t off = uint32_t(p - w.base);
-  const uint32_t dw = __builtin_amdgcn_readlane(off < 256u ? w.cur : w.nxt, int((off & 255u) >> 2));
+  // uniform branch: only touch nxt (possibly still in flight) when needed
+  uint32_t dw;
+  if (off < 256u) dw = __builtin_amdgcn_readlane(w.cur, int(off >> 2));
+  else dw = __builtin_amdgcn_readlane(w.nxt, int((off & 255u) >> 2));
   return (dw >> (8u * uint32_t(p & 3u))) & 0xFFu;
 }
 
@@ -93,42 +96,156 @@ __device__ __forceinline__ void copy_fwd(uintptr_t d, uintptr_t s, uint32_t len,
   asm volatile("" ::: "memory");
 }
 
-// out[op+i] = out[op-offset+i] with LZ77 overlap semantics
-__device__ __forceinline__ void copy_match(uintptr_t dst, uint32_t op, uint32_t offset,
-                                           uint32_t len, int lane) {
-  asm volatile("" ::: "memory");
-  if (offset == 0) {  // the reference writes zeros (lz4.c:2026 / LZ4_memcpy_using_offset)
-    for (uint32_t i = lane; i < len; i += 64u) stb(dst + op + i, 0u);
-  } else if (offset >= len || offset >= 64u) {
-    // chunks of min(offset, 256) bytes never read bytes written in the same chunk
-    const uint32_t chunk = offset >= 256u ? 256u : (offset >= 64u ? 64u : offset);
-    for (uint32_t base = 0; base < len; base += chunk) {
+// ------------------------------------------------------ output history ring
+// Each wavefront decodes into an 8 KiB LDS ring holding the newest output
+// bytes and streams it to HBM in 4 KiB pieces with 16-byte stores.  Matches
+// reaching <= kRingReach back (the common case) are served from LDS; longer
+// ones, and linked-block matches into the previous blocks, read the
+// already-flushed output from global memory.  Literals come from the input
+// register window (cross-lane ds_bpermute), so in the steady state a sequence
+// touches HBM only through the window prefetch and the ring flush.
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4v lds_u32x4;
+typedef __attribute__((address_space(1))) u32x4v g_u32x4;
+constexpr uint32_t kRing = 8192;
+constexpr uint32_t kRingMask = kRing - 1u;
+constexpr uint32_t kFlush = 4096;               // bytes per streamed piece
+constexpr uint32_t kRingReach = kRing - 256u;   // max offset served from LDS
+constexpr int kDecWaves = 4;                    // wavefronts per workgroup
+
+struct OutRing {
+  uintptr_t dst;      // block output in global memory
+  lds_u8 *ring;
+  uint32_t flushed;   // bytes [0, flushed) are in global memory
+};
+
+// copy output bytes [from, to) from the ring to global memory
+__device__ __forceinline__ void ring_store(const OutRing &o, uint32_t from, uint32_t to, int lane) {
+  uint32_t x = from;
+  if (((o.dst + from) & 15u) == 0) {
+    const uint32_t vend = from + ((to - from) & ~15u);
+    for (uint32_t y = from + uint32_t(lane) * 16u; y < vend; y += 1024u)
+      *(g_u32x4 *)(o.dst + y) = *(const lds_u32x4 *)(o.ring + (y & kRingMask));
+    x = vend;
+  }
+  for (uint32_t y = x + uint32_t(lane); y < to; y += 64u) stb(o.dst + y, o.ring[y & kRingMask]);
+}
+
+// after output reached `op`: stream every complete 4 KiB piece
+__device__ __forceinline__ void ring_advance(OutRing &o, uint32_t op, int lane) {
+  while (op - o.flushed >= kFlush) {
+    ring_store(o, o.flushed, o.flushed + kFlush, lane);
+    o.flushed += kFlush;
+  }
+}
+
+__device__ __forceinline__ void ring_finish(OutRing &o, uint32_t op, int lane) {
+  ring_advance(o, op, lane);
+  if (op > o.flushed) ring_store(o, o.flushed, op, lane);
+  o.flushed = op;
+}
+
+// window bytes rel0 + lane (rel0 wave-uniform, rel0 + 64 <= 512): cross-lane
+// gather of the dword holding each; nxt (possibly still in flight) is only
+// touched when the range reaches it
+__device__ __forceinline__ uint32_t win_gather(uint32_t rel0, uint32_t cur, uint32_t nxt, int lane) {
+  const uint32_t rel = rel0 + uint32_t(lane);
+  const uint32_t dw = rel >> 2;
+  const int addr = int((dw & 63u) << 2);
+  uint32_t v;
+  if (rel0 + 63u < 256u) {
+    v = uint32_t(__builtin_amdgcn_ds_bpermute(addr, int(cur)));
+  } else if (rel0 >= 256u) {
+    v = uint32_t(__builtin_amdgcn_ds_bpermute(addr, int(nxt)));
+  } else {
+    const uint32_t a = uint32_t(__builtin_amdgcn_ds_bpermute(addr, int(cur)));
+    const uint32_t b = uint32_t(__builtin_amdgcn_ds_bpermute(addr, int(nxt)));
+    v = dw < 64u ? a : b;
+  }
+  return (v >> (8u * (rel & 3u))) & 0xFFu;
+}
+
+// make the window cover input bytes [p, p+64) (p wave-uniform)
+__device__ __forceinline__ void win_cover(InWin &w, uintptr_t p, int lane) {
+  if (p >= w.base && p + 64u <= w.base + 512u) return;
+  if (p >= w.base + 256u && p < w.base + 512u) {  // slide by 256, prefetching the next half
+    w.base += 256u;
+    w.cur = w.nxt;
+    w.nxt = ld_dw(w.base + 256u + 4u * lane, w.lim);
+  } else {
+    win_load(w, p & ~uintptr_t(3), lane);
+  }
+}
+
+// literal run: input [p, p+n) -> output [op, op+n) through the ring
+__device__ __forceinline__ void ring_literals(OutRing &o, InWin &w, uintptr_t p, uint32_t op,
+                                              uint32_t n, int lane) {
+  for (uint32_t base = 0; base < n; base += 64u) {
+    const uintptr_t q = p + base;
+    win_cover(w, q, lane);
+    const uint32_t v = win_gather(uint32_t(q - w.base), w.cur, w.nxt, lane);
+    if (base + uint32_t(lane) < n) o.ring[(op + base + uint32_t(lane)) & kRingMask] = uint8_t(v);
+    ring_advance(o, op + (n - base < 64u ? n : base + 64u), lane);
+  }
+}
+
+// match: out[op+i] = out[op-off+i], i < len, with LZ77 overlap semantics
+// (offset 0 writes zeros like the reference, lz4.c:2026).  GLOBAL: some
+// source bytes are older than the ring (far offsets, or linked-block history
+// in front of dst) and come from global memory; the LDS-only instantiation
+// never waits on vector memory.
+template <bool GLOBAL>
+__device__ __forceinline__ void ring_match_t(OutRing &o, uint32_t op, uint32_t off, uint32_t len,
+                                             int lane) {
+  const bool far = GLOBAL && off > kRingReach;
+  const long back = long(op) - long(off);
+  auto rd = [&](long q) -> uint32_t {
+    if (GLOBAL && (far || q < 0)) return ldb(o.dst + q);
+    return uint32_t(o.ring[uint32_t(q) & kRingMask]);
+  };
+  if (off == 0) {
+    for (uint32_t base = 0; base < len; base += 64u) {
+      if (base + uint32_t(lane) < len) o.ring[(op + base + uint32_t(lane)) & kRingMask] = 0;
+      ring_advance(o, op + (len - base < 64u ? len : base + 64u), lane);
+    }
+  } else if (off < 64u) {  // small period: each 64-byte step reads the off bytes before it
+    const uint32_t lm = uint32_t(lane) % off;
+    for (uint32_t base = 0; base < len; base += 64u) {
+      const uint32_t v = rd(back + long(base) + long(lm));
+      if (base + uint32_t(lane) < len) o.ring[(op + base + uint32_t(lane)) & kRingMask] = uint8_t(v);
+      ring_advance(o, op + (len - base < 64u ? len : base + 64u), lane);
+    }
+  } else {  // steps of min(off, 256) never read bytes written in the same step
+    const uint32_t step = off >= 256u ? 256u : 64u;
+    for (uint32_t base = 0; base < len; base += step) {
       uint32_t v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint32_t i = base + lane + 64u * j;
-        v[j] = (lane + 64u * j < chunk && i < len) ? ldb(dst + op - offset + i) : 0u;
+        const uint32_t i = base + uint32_t(lane) + 64u * j;
+        v[j] = (64u * j < step && i < len) ? rd(back + long(i)) : 0u;
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint32_t i = base + lane + 64u * j;
-        if (lane + 64u * j < chunk && i < len) stb(dst + op + i, v[j]);
+        const uint32_t i = base + uint32_t(lane) + 64u * j;
+        if (64u * j < step && i < len) o.ring[(op + i) & kRingMask] = uint8_t(v[j]);
       }
-      asm volatile("" ::: "memory");
-    }
-  } else {  // small period: out[op+i] = out[op-offset + (i mod offset)]
-    const uint32_t lane_mod = uint32_t(lane) % offset, step_mod = 64u % offset;
-    uint32_t cur = 0;
-    for (uint32_t base = 0; base < len; base += 64u) {
-      uint32_t m = lane_mod + cur;
-      if (m >= offset) m -= offset;
-      const uint32_t i = base + lane;
-      if (i < len) stb(dst + op + i, ldb(dst + op - offset + m));
-      cur += step_mod;
-      if (cur >= offset) cur -= offset;
+      ring_advance(o, op + (len - base < step ? len : base + step), lane);
     }
   }
-  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void ring_match(OutRing &o, uint32_t op, uint32_t off, uint32_t len,
+                                           int lane) {
+  if (off <= kRingReach && off <= op) {
+    ring_match_t<false>(o, op, off, len, lane);
+  } else {
+    // flushed / previous-block output is read back by this same wavefront: a
+    // workgroup-scope fence (wait for its stores) suffices -- __threadfence()
+    // would write back the whole L2 for cross-XCD coherence
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    ring_match_t<true>(o, op, off, len, lane);
+  }
 }
 
 // ---------------------------------------------------------- block decoder
@@ -136,7 +253,7 @@ __device__ __forceinline__ void copy_match(uintptr_t dst, uint32_t op, uint32_t 
 // caller's buffer (realcap) is too small.  `hist` = bytes of frame history
 // directly in front of dst (linked frames), selecting noDict /
 // withSmallPrefix / withPrefix64k exactly like LZ4_decompress_safe_usingDict.
-__device__ int decode_block(uintptr_t src, int csize, uintptr_t dst, int vcap, int realcap,
+__device__ int decode_block(uintptr_t src, int csize, OutRing &o, int vcap, int realcap,
                             int hist, int lane) {
   const int iend = csize, oend = vcap;
   const bool prefix64k = hist >= 65535;
@@ -167,12 +284,12 @@ __device__ int decode_block(uintptr_t src, int csize, uintptr_t dst, int vcap, i
   };
   auto lit = [&](uint32_t n) -> bool {
     if (op + int(n) > realcap) return false;
-    copy_fwd(dst + op, src + ip, n, lane);
+    ring_literals(o, w, src + uintptr_t(ip), uint32_t(op), n, lane);
     return true;
   };
   auto mat = [&](uint32_t n) -> bool {
     if (op + int(n) > realcap) return false;
-    copy_match(dst, uint32_t(op), uint32_t(offset), n, lane);
+    ring_match(o, uint32_t(op), uint32_t(offset), n, lane);
     return true;
   };
 
@@ -277,6 +394,7 @@ safe_decode:
     op = cpy;
   }
 #undef RDK_B
+  ring_finish(o, uint32_t(op), lane);
   return op;
 }
 
@@ -286,9 +404,12 @@ struct DevReader {
   __device__ uint32_t operator()(uint64_t i) const { return ldb(p + i); }
 };
 
+// Also appends the (frame, block) items of every regular frame to a compact
+// work list, so the block kernel's wavefronts only ever see real blocks.
 __global__ void lz4f_walk_kernel(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
                                  const uint32_t *__restrict__ in_lens, uint32_t n,
-                                 FrameState *__restrict__ fs, BlockDesc *__restrict__ bd) {
+                                 FrameState *__restrict__ fs, BlockDesc *__restrict__ bd,
+                                 uint32_t *__restrict__ work_count, uint32_t *__restrict__ work) {
   const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n) return;
   FrameWalker<DevReader> wk{DevReader{reinterpret_cast<uintptr_t>(in) + in_offs[f]}, in_lens[f]};
@@ -306,12 +427,16 @@ __global__ void lz4f_walk_kernel(const uint8_t *__restrict__ in, const uint64_t 
   if ((wk.fi.flags & F_LINKED) || k > uint32_t(kMaxDesc)) wk.fi.flags |= F_SEQ;
   fs[f].fi = wk.fi;
   fs[f].seq_result = 0;
+  if (wk.fi.status == 0 && !(wk.fi.flags & (F_SKIPPABLE | F_SEQ)) && wk.fi.nblocks) {
+    const uint32_t at = atomicAdd(work_count, wk.fi.nblocks);
+    for (uint32_t j = 0; j < wk.fi.nblocks; ++j) work[at + j] = f * uint32_t(kMaxDesc) + j;
+  }
 }
 
 // one block: raw copy or LZ4 decode, with the block checksum check first
 // (dstage_getCBlock verifies XXH32 before decoding, lz4frame.c:1596-1608)
 __device__ int run_block(const BlockInfo &b, uintptr_t frame, uintptr_t dst, uint32_t max_block,
-                         int realcap, int hist, int lane) {
+                         int realcap, int hist, lds_u8 *ring, int lane) {
   const uintptr_t src = frame + b.src_off;
   if (b.flags & B_RAW) {
     if (int(b.csize) > realcap) return -2;
@@ -326,7 +451,8 @@ __device__ int run_block(const BlockInfo &b, uintptr_t frame, uintptr_t dst, uin
     uint32_t h = lane == 0 ? xxh32_lane(src, b.csize, 0) : 0u;
     if (uni(h) != b.xxh) return -1;
   }
-  return decode_block(src, int(b.csize), dst, int(max_block), realcap, hist, lane);
+  OutRing o{dst, ring, 0u};
+  return decode_block(src, int(b.csize), o, int(max_block), realcap, hist, lane);
 }
 
 __device__ __forceinline__ int realcap_at(uint64_t cap, uint64_t at, uint32_t limit) {
@@ -336,39 +462,43 @@ __device__ __forceinline__ int realcap_at(uint64_t cap, uint64_t at, uint32_t li
 }
 
 // independent blocks of regular frames: one wavefront per (frame, block)
-__global__ __launch_bounds__(256) void lz4f_blocks_kernel(
+__global__ __launch_bounds__(64 * kDecWaves) void lz4f_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs, uint8_t *out,
     const uint64_t *__restrict__ out_offs, const uint32_t *__restrict__ out_caps, uint32_t n,
-    const FrameState *__restrict__ fs, BlockDesc *__restrict__ bd) {
+    const FrameState *__restrict__ fs, BlockDesc *__restrict__ bd,
+    const uint32_t *__restrict__ work_count, const uint32_t *__restrict__ work) {
+  __shared__ __attribute__((aligned(16))) uint8_t rings[kDecWaves][kRing];
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
+  lds_u8 *ring = (lds_u8 *)rings[uni(threadIdx.x >> 6)];
   const uint32_t gw = blockIdx.x * wpb + uni(threadIdx.x >> 6);
-  const uint64_t items = uint64_t(n) * kMaxDesc;
-  for (uint64_t it = gw; it < items; it += uint64_t(gridDim.x) * wpb) {
-    const uint32_t f = uint32_t(it / kMaxDesc), k = uint32_t(it % kMaxDesc);
-    const uint32_t status = uni(uint32_t(fs[f].fi.status));
-    const uint32_t flags = uni(fs[f].fi.flags);
-    const uint32_t nblocks = uni(fs[f].fi.nblocks);
-    if (status != 0 || (flags & (F_SKIPPABLE | F_SEQ)) || k >= nblocks) continue;
+  const uint32_t items = uni(*work_count);
+  (void)n;
+  for (uint32_t it = gw; it < items; it += gridDim.x * wpb) {
+    const uint32_t wi = uni(work[it]);
+    const uint32_t f = wi / uint32_t(kMaxDesc), k = wi % uint32_t(kMaxDesc);
     const uint32_t mb = uni(fs[f].fi.max_block);
     const uintptr_t frame = reinterpret_cast<uintptr_t>(in) + in_offs[f];
     const uintptr_t obase = reinterpret_cast<uintptr_t>(out) + out_offs[f];
     BlockInfo b = bd[size_t(f) * kMaxDesc + k].b;
     b.src_off = uni(b.src_off); b.csize = uni(b.csize); b.flags = uni(b.flags); b.xxh = uni(b.xxh);
     const uint64_t slot = uint64_t(k) * mb;
-    const int r = run_block(b, frame, obase + slot, mb, realcap_at(out_caps[f], slot, mb), 0, lane);
+    const int r = run_block(b, frame, obase + slot, mb, realcap_at(out_caps[f], slot, mb), 0, ring,
+                            lane);
     if (lane == 0) bd[size_t(f) * kMaxDesc + k].result = r;
   }
 }
 
 // linked frames and frames with more than kMaxDesc blocks: one wavefront
 // decodes the whole frame in stream order into contiguous output
-__global__ __launch_bounds__(256) void lz4f_seq_kernel(
+__global__ __launch_bounds__(64 * kDecWaves) void lz4f_seq_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
     const uint32_t *__restrict__ out_caps, uint32_t n, FrameState *__restrict__ fs) {
+  __shared__ __attribute__((aligned(16))) uint8_t rings[kDecWaves][kRing];
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
+  lds_u8 *ring = (lds_u8 *)rings[uni(threadIdx.x >> 6)];
   const uint32_t gw = blockIdx.x * wpb + uni(threadIdx.x >> 6);
   for (uint32_t f = gw; f < n; f += gridDim.x * wpb) {
     const uint32_t status = uni(uint32_t(fs[f].fi.status));
@@ -388,7 +518,7 @@ __global__ __launch_bounds__(256) void lz4f_seq_kernel(
       b.src_off = uni(b.src_off); b.csize = uni(b.csize); b.flags = uni(b.flags); b.xxh = uni(b.xxh);
       const int hist = linked ? int(produced < 65536u ? produced : 65536u) : 0;
       const int r = run_block(b, frame, obase + produced, mb, realcap_at(cap, produced, mb), hist,
-                              lane);
+                              ring, lane);
       if (r < 0) { res = r; break; }
       produced += uint64_t(r);
     }
@@ -480,14 +610,21 @@ int lz4f_decompress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_off
   if (!n) return 0;
   const size_t fs_bytes = (size_t(n) * sizeof(FrameState) + 255) & ~size_t(255);
   const size_t bd_bytes = size_t(n) * kMaxDesc * sizeof(BlockDesc);
-  int rc = ensure_dev(c, 1, fs_bytes + bd_bytes);
+  const size_t wk_bytes = 256 + size_t(n) * kMaxDesc * sizeof(uint32_t);
+  int rc = ensure_dev(c, 1, fs_bytes + bd_bytes + wk_bytes);
   if (rc) return rc;
   FrameState *fs = reinterpret_cast<FrameState *>(c->d_stage[1]);
   BlockDesc *bd = reinterpret_cast<BlockDesc *>(c->d_stage[1] + fs_bytes);
+  uint32_t *work_count = reinterpret_cast<uint32_t *>(c->d_stage[1] + fs_bytes + bd_bytes);
+  uint32_t *work = work_count + 64;
+  RDK_HIP_CHECK(hipMemsetAsync(work_count, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(lz4f_walk_kernel, dim3((n + 63) / 64), dim3(64), 0, s, d_in, d_in_offs,
-                     d_in_lens, n, fs, bd);
-  hipLaunchKernelGGL(lz4f_blocks_kernel, dim3(grid_waves(uint64_t(n) * kMaxDesc, 4)), dim3(256), 0,
-                     s, d_in, d_in_offs, d_out, d_out_offs, d_out_caps, n, fs, bd);
+                     d_in_lens, n, fs, bd, work_count, work);
+  // persistent grid: LDS (kDecWaves rings of 8 KiB) allows 5 workgroups per CU
+  const uint64_t want = (uint64_t(n) * kMaxDesc + kDecWaves - 1) / kDecWaves;
+  const unsigned bgrid = unsigned(want < 1280u ? (want ? want : 1u) : 1280u);
+  hipLaunchKernelGGL(lz4f_blocks_kernel, dim3(bgrid), dim3(64 * kDecWaves), 0, s, d_in,
+                     d_in_offs, d_out, d_out_offs, d_out_caps, n, fs, bd, work_count, work);
   hipLaunchKernelGGL(lz4f_seq_kernel, dim3(grid_waves(n, 4)), dim3(256), 0, s, d_in, d_in_offs,
                      d_in_lens, d_out, d_out_offs, d_out_caps, n, fs);
   hipLaunchKernelGGL(lz4f_finish_kernel, dim3(grid_waves(n, 4)), dim3(256), 0, s, d_out,

@@ -126,6 +126,19 @@ int rdk_hip_lz4f_compress(const void *d_in, const uint64_t *d_in_offs,
                           const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, int level, void *stream);
 
+/* Throughput-mode LZ4F compression: same arguments, frame format, prefs
+ * ({blockIndependent}, 64 KB blocks, no checksums) and raw-block fallback
+ * (lz4frame.c:739-761) as rdk_hip_lz4f_compress, but the match search is the
+ * engine's own wavefront-parallel one (dense LZ4_hash4 table, 64 positions per
+ * step), not an emulation of LZ4_compress_generic.  Frames decode with the
+ * reference's rd_kafka_lz4_decompress (rdkafka_lz4.c:167) to the input;
+ * they are not byte-identical to rd_kafka_lz4_compress's (rdkafka_lz4.c:329);
+ * the compression ratio is within 5 % of it (tests/test_gpu_lz4.py). */
+int rdk_hip_lz4f_compress_fast(const void *d_in, const uint64_t *d_in_offs,
+                               const uint32_t *d_in_lens, void *d_out,
+                               const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                               uint32_t n, void *stream);
+
 /* LZ4F decompression of n independent frames (rd_kafka_lz4_decompress
  * semantics per frame, proper HC).  Frame i decodes into
  * d_out + d_out_offs[i] with capacity d_out_caps[i]; d_out_lens[i] gets the

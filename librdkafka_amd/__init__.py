@@ -44,7 +44,8 @@ EXPORTED_SYMBOLS = (
     "crc32c", "crc32c_global_init", "rd_slice_crc32c", "rd_kafka_lz4_compress",
     "rd_kafka_lz4_decompress", "rdk_hip_init", "rdk_hip_last_error", "rdk_hip_version",
     "rdk_hip_crc32c_ranges", "rdk_hip_msgset_v2_crc", "rdk_hip_lz4f_compress_bound",
-    "rdk_hip_lz4f_compress", "rdk_hip_lz4f_decompress", "rdk_hip_gen_v2_batches",
+    "rdk_hip_lz4f_compress", "rdk_hip_lz4f_compress_fast", "rdk_hip_lz4f_decompress",
+    "rdk_hip_gen_v2_batches",
     "rdk_hip_gen_json",
 )
 
@@ -93,6 +94,8 @@ def lib():
         L.rdk_hip_lz4f_compress_bound.argtypes = [sz]
         L.rdk_hip_lz4f_compress.restype = i32
         L.rdk_hip_lz4f_compress.argtypes = [vp, vp, vp, vp, vp, vp, u32, i32, vp]
+        L.rdk_hip_lz4f_compress_fast.restype = i32
+        L.rdk_hip_lz4f_compress_fast.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp]
         L.rdk_hip_lz4f_decompress.restype = i32
         L.rdk_hip_lz4f_decompress.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
     L.rdk_hip_gen_v2_batches.restype = i32
@@ -269,6 +272,15 @@ def lz4f_compress_batch(src, in_offs, in_lens, dst, out_offs, out_lens, level=0,
     _check(lib().rdk_hip_lz4f_compress(_ptr(src), _ptr(in_offs), _ptr(in_lens), _ptr(dst),
                                        _ptr(out_offs), _ptr(out_lens), int(in_offs.numel()),
                                        level, _stream(stream)), "lz4f_compress")
+
+
+def lz4f_compress_fast_batch(src, in_offs, in_lens, dst, out_offs, out_lens, stream=None):
+    """Throughput-mode LZ4F compression (csrc/lz4_encode_fast.hip): same frame
+    format and prefs as rd_kafka_lz4_compress, reference-decodable, ratio
+    within 5 % of the reference's; not byte-identical to its frames."""
+    _check(lib().rdk_hip_lz4f_compress_fast(_ptr(src), _ptr(in_offs), _ptr(in_lens), _ptr(dst),
+                                            _ptr(out_offs), _ptr(out_lens), int(in_offs.numel()),
+                                            _stream(stream)), "lz4f_compress_fast")
 
 
 def lz4f_decompress_batch(src, in_offs, in_lens, dst, out_offs, out_caps, out_lens, status,

@@ -343,6 +343,10 @@ size_t lz4f_compress_bound(size_t len) {
   return 7u + nb * size_t(kSlot) + 4u;
 }
 
+void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
+                          uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                          uint32_t n, hipStream_t s);
+
 int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
                          const uint32_t *d_in_lens, uint8_t *d_out, const uint64_t *d_out_offs,
                          uint32_t *d_out_lens, uint32_t n, int accel, hipStream_t s) {
@@ -352,11 +356,22 @@ int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
   hipLaunchKernelGGL(lz4_compress_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
                      d_in_lens, d_out, d_out_offs, n, accel);
-  hipLaunchKernelGGL(lz4f_assemble_kernel, dim3(n < 8192u ? n : 8192u), dim3(256), 0, s, d_in,
-                     d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n);
+  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;
 }
+
+void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
+                          uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                          uint32_t n, hipStream_t s) {
+  hipLaunchKernelGGL(lz4f_assemble_kernel, dim3(n < 8192u ? n : 8192u), dim3(256), 0, s, d_in,
+                     d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n);
+}
+
+int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
+                              const uint32_t *d_in_lens, uint8_t *d_out,
+                              const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
+                              hipStream_t s);
 
 }  // namespace rdk
 
@@ -378,4 +393,18 @@ RDK_API int rdk_hip_lz4f_compress(const void *d_in, const uint64_t *d_in_offs,
   const int accel = level < 0 ? -level + 1 : 1;  // LZ4F_compressBlock, lz4frame.c:766
   return lz4f_compress_device(c, static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
                               static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n, accel, s);
+}
+
+RDK_API int rdk_hip_lz4f_compress_fast(const void *d_in, const uint64_t *d_in_offs,
+                                       const uint32_t *d_in_lens, void *d_out,
+                                       const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                                       uint32_t n, void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_in || !d_in_offs || !d_in_lens || !d_out || !d_out_offs || !d_out_lens)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  return lz4f_compress_fast_device(static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
+                                   static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n,
+                                   static_cast<hipStream_t>(stream));
 }

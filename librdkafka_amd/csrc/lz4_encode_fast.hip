@@ -1,0 +1,401 @@
+// lz4_encode_fast.hip -- throughput-mode LZ4F compression on gfx950.
+//
+// Same frame format and block independence as rd_kafka_lz4_compress
+// (src/rdkafka_lz4.c:329-442: prefs {blockIndependent, level}, 64 KiB blocks,
+// no checksums, LZ4F_makeBlock's raw fallback lz4frame.c:739-761), but the
+// match search is restructured for a wavefront instead of emulating the
+// sequential LZ4_compress_generic loop (lz4.c:789-1177) step by step:
+//
+//   * positions are processed in rounds of 64 (one per lane).  Every position
+//     <= n-12 is hashed with LZ4_hash4 (lz4.c:631) into a 2^13-entry u16 table
+//     in LDS that holds the LATEST earlier position per hash (dense insertion,
+//     the reference inserts only the positions it probes);
+//   * a lane's candidate is the table entry as of the start of its round; the
+//     lane verifies MINMATCH bytes, measures up to 16 match bytes and up to 4
+//     catch-up bytes (lz4.c:957) from two 24-byte register windows (its own
+//     position and the candidate's), so one round costs two gathers, not a
+//     chain of dependent loads per sequence;
+//   * the greedy parse (first verified position at or after the end of the
+//     previous match) is scalar: a ctz over the round's match ballot and one
+//     readlane per sequence; only matches longer than 16 bytes go back to
+//     memory (64 bytes per wave step);
+//   * sequences are collected 64 at a time in two VGPRs and emitted together:
+//     a wave prefix sum places every sequence, each lane writes its token,
+//     length bytes, literals and offset (LZ4 block format, lz4.c:961-1073).
+//
+// The output is a valid LZ4 frame that the reference decoder
+// (rd_kafka_lz4_decompress, rdkafka_lz4.c:167) decodes to the input; it is NOT
+// byte-identical to the reference's frame (use the exact engine in
+// lz4_encode.hip for that).  The compression ratio is pinned against the
+// reference's by tests/test_gpu_lz4.py (north_star: within 5 %).
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "lz4_device.h"
+
+namespace rdk {
+
+void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
+                          uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                          uint32_t n, hipStream_t s);
+
+namespace {
+
+constexpr int kFastMaxItems = 64;              // block slots per frame per pass
+constexpr uint32_t kFastSlot = kLz4Block + 4;  // worst-case bytes per block in a frame
+constexpr uint32_t kFastHashLog = 13;
+constexpr int kFastLen = 28;                   // match bytes measured from registers
+
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+typedef __attribute__((address_space(1))) const u32x4a g_cu32x4a;
+typedef __attribute__((address_space(1))) const u32x2a g_cu32x2a;
+
+__device__ __forceinline__ uint32_t hash4(uint32_t seq) {  // LZ4_hash4, lz4.c:631
+  return (seq * 2654435761u) >> (32 - kFastHashLog);
+}
+
+// All block reads go through a raw buffer resource spanning the block's
+// dwords [lo, hi): MUBUF range checking is per dword, so a dword outside the
+// block (or a lane parked at kNoLoad) reads 0 and touches no memory.  Loads
+// are issued unconditionally, which keeps the compiler's vmcnt bookkeeping
+// exact and lets the next round's loads stay in flight.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kNoLoad = 0x80000000u;
+
+__device__ __forceinline__ rsrc_t block_rsrc(uintptr_t lo, uintptr_t hi) {
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(lo), 0, int(hi - lo),
+                                           0x00020000);
+}
+
+// nine dwords at block offset a-4 .. a+28 (a 4-aligned, relative to lo).
+// The dword before a is its own load: a vector load that starts below the
+// resource (a-4 wraps) reads as zero as a whole.
+__device__ __forceinline__ void load9(rsrc_t r, uint32_t a, uint32_t d[9]) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  d[0] = __builtin_amdgcn_raw_buffer_load_b32(r, a - 4u, 0, 0);
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, a, 0, 0);
+  const u4 w = __builtin_amdgcn_raw_buffer_load_b128(r, a + 16u, 0, 0);
+  d[1] = v.x; d[2] = v.y; d[3] = v.z; d[4] = v.w;
+  d[5] = w.x; d[6] = w.y; d[7] = w.z; d[8] = w.w;
+}
+
+// five dwords at block offset a .. a+16
+__device__ __forceinline__ void load5(rsrc_t r, uint32_t a, uint32_t d[5]) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, a, 0, 0);
+  d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  d[4] = __builtin_amdgcn_raw_buffer_load_b32(r, a + 16u, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_t &total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(x, d);
+    if (lane >= d) x += t;
+  }
+  total = __builtin_amdgcn_readlane(x, 63);
+  return x - v;
+}
+
+// equal bytes a[i]==b[i] for i in [0, limit), 64 per wave step
+__device__ __forceinline__ int wave_count_fwd(uintptr_t a, uintptr_t b, int limit, int lane) {
+  int cnt = 0;
+  while (cnt < limit) {
+    const int l = cnt + lane;
+    const bool ok = l < limit && ldb(a + l) == ldb(b + l);
+    const uint64_t m = ballot(ok);
+    const int run = m == ~0ull ? 64 : __builtin_ctzll(~m);
+    cnt += run;
+    if (run < 64) break;
+  }
+  return cnt;
+}
+
+__device__ __forceinline__ void wave_copy_bytes(uintptr_t d, uintptr_t s, uint32_t len, int lane) {
+  for (uint32_t base = 0; base < len; base += 256u) {
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = base + lane + 64u * j;
+      v[j] = i < len ? ldb(s + i) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = base + lane + 64u * j;
+      if (i < len) stb(d + i, v[j]);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {  // 255-run encoding length
+  return v >= 15u ? (v - 15u) / 255u + 1u : 0u;
+}
+
+__device__ __forceinline__ uintptr_t put_len(uintptr_t p, uint32_t v) {  // v >= 15
+  uint32_t r = v - 15u;
+  for (; r >= 255u; r -= 255u) stb(p++, 255u);
+  stb(p++, r);
+  return p;
+}
+
+constexpr uint32_t kShortLit = 16;  // literal runs copied by their own lane
+
+struct BlockCtx {
+  uintptr_t src, dst;
+  rsrc_t r;            // the block's dwords
+  uint32_t sa;         // src & 3: byte offset of position 0 inside the resource
+  int n, mfl, mlim, olimit;
+  int anchor, p, op, ns, batch_anchor;
+  uint32_t seqA, seqB; // lane j: sequence j of the current batch (lit | ml<<16, offset)
+};
+
+// Emit the b.ns collected sequences at dst+op.  Returns false when the block
+// would not fit in olimit bytes (stored raw).
+__device__ bool emit_batch(BlockCtx &b, int lane) {
+  const bool on = lane < b.ns;
+  const uint32_t lit = on ? (b.seqA & 0xFFFFu) : 0u;
+  const uint32_t ml = on ? (b.seqA >> 16) : 0u;
+  const uint32_t sz = on ? 3u + lit + ext_bytes(lit) + ext_bytes(ml - 4u) : 0u;
+  uint32_t tot_sz, tot_span;
+  const uint32_t o = wave_excl_scan(sz, lane, tot_sz);
+  const uint32_t a = wave_excl_scan(lit + ml, lane, tot_span);
+  (void)tot_span;
+  // keep room for the shortest possible last-literals token (lz4.c:1146)
+  if (b.op + int(tot_sz) + 1 > b.olimit) return false;
+  const uint32_t lstart = uint32_t(b.batch_anchor) + a;
+  // short literal runs come from one 20-byte window per lane (one load)
+  const uint32_t al = lstart + b.sa;
+  uint32_t w[5];
+  load5(b.r, (on && lit && lit <= kShortLit) ? (al & ~3u) : kNoLoad, w);
+  if (on) {
+    uintptr_t p = b.dst + uint32_t(b.op) + o;
+    const uint32_t mc = ml - 4u;
+    stb(p++, ((lit < 15u ? lit : 15u) << 4) | (mc < 15u ? mc : 15u));
+    if (lit >= 15u) p = put_len(p, lit);
+    if (lit <= kShortLit) {
+      const uint32_t sh = al & 3u;
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+#pragma unroll
+      for (uint32_t k = 0; k < kShortLit; ++k)
+        if (k < lit) stb(p + k, v[k >> 2] >> (8u * (k & 3u)));
+    }
+    p += lit;
+    stb(p, b.seqB & 0xFFu);
+    stb(p + 1, (b.seqB >> 8) & 0xFFu);
+    p += 2;
+    if (mc >= 15u) put_len(p, mc);
+  }
+  // long literal runs: the whole wave copies them one at a time
+  uint64_t longm = ballot(on && lit > kShortLit);
+  while (longm) {
+    const int j = __builtin_ctzll(longm);
+    longm &= longm - 1;
+    const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
+    const uint32_t jo = __builtin_amdgcn_readlane(o, j);
+    const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
+    wave_copy_bytes(b.dst + uint32_t(b.op) + jo + 1u + ext_bytes(jl), b.src + js, jl, lane);
+  }
+  b.op += int(tot_sz);
+  b.ns = 0;
+  b.batch_anchor = b.anchor;
+  return true;
+}
+
+// One round of 64 positions in flight: the lane's own 40-byte window, its
+// candidate (or -1) and the candidate's window.
+struct Round {
+  uint32_t d[9];
+  uint32_t t[9];
+  int c;
+};
+
+__device__ __forceinline__ void round_load(const BlockCtx &b, Round &x, int R, int lane) {
+  const int i = R + lane;
+  load9(b.r, i <= b.mfl ? ((uint32_t(i) + b.sa) & ~3u) : kNoLoad, x.d);
+}
+
+// hash + table for the round at R (window x.d arrived), then issue the
+// candidate gather for the lanes the parse may still need (i >= p)
+__device__ __forceinline__ void round_lookup(const BlockCtx &b, Round &x, int R, lds_u16 *table,
+                                             int lane) {
+  const int i = R + lane;
+  const bool act = i <= b.mfl;
+  const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
+  const uint32_t s0 = __builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi);
+  const uint32_t h = hash4(s0);
+  const int c = act ? int(table[h]) : 0;
+  // insert position i; the largest position of a hash wins (deterministic)
+  if (act) table[h] = uint16_t(i);
+  for (;;) {
+    const bool fix = act && int(table[h]) < i;
+    if (!ballot(fix)) break;
+    if (fix) table[h] = uint16_t(i);
+  }
+  x.c = (act && i >= b.p && c < i) ? c : -1;
+  load9(b.r, x.c >= 0 ? ((uint32_t(c) + b.sa) & ~3u) : kNoLoad, x.t);
+}
+
+// measure the round's matches (windows arrived), then parse it greedily
+__device__ __forceinline__ bool round_parse(BlockCtx &b, const Round &x, int R, int lane) {
+  const int i = R + lane;
+  const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
+  const uint32_t shc = (uint32_t(x.c) + b.sa) & 3u;
+  const bool valid = x.c >= 0 && i >= b.p &&
+                     __builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi) ==
+                         __builtin_amdgcn_alignbyte(x.t[2], x.t[1], shc);
+  int len = kFastLen;
+#pragma unroll
+  for (int k = 6; k >= 1; --k) {
+    const uint32_t y = __builtin_amdgcn_alignbyte(x.d[k + 2], x.d[k + 1], shi) ^
+                       __builtin_amdgcn_alignbyte(x.t[k + 2], x.t[k + 1], shc);
+    if (y) len = 4 * k + (__builtin_ctz(y) >> 3);
+  }
+  if (len > b.mlim - i) len = b.mlim - i;
+  const uint32_t xb = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi) ^
+                      __builtin_amdgcn_alignbyte(x.t[1], x.t[0], shc);
+  const uint32_t bk = xb ? uint32_t(__builtin_clz(xb) >> 3) : 4u;
+  const uint32_t pack = uint32_t(len) | (bk << 6) | (uint32_t(i - x.c) << 9);
+  const uint64_t vm = ballot(valid);
+#ifdef RDK_FAST_DEBUG
+  if (R == 0 && lane < 4)
+    printf("lane %d c %d valid %d shi %u shc %u d %08x %08x %08x t %08x %08x %08x len %d\n", lane,
+           x.c, int(valid), shi, shc, x.d[0], x.d[1], x.d[2], x.t[0], x.t[1], x.t[2], len);
+#endif
+  for (;;) {
+    const int rel = b.p - R;
+    if (rel >= 64) break;
+    const uint64_t m = rel > 0 ? (vm & (~0ull << rel)) : vm;
+    if (!m) break;
+    const int q = __builtin_ctzll(m);
+    const uint32_t pk = __builtin_amdgcn_readlane(pack, q);
+    const int qi = R + q;
+    const int off = int(pk >> 9);
+    int L = int(pk & 63u);
+    int bkq = int((pk >> 6) & 7u);
+    bkq = min(bkq, min(qi - b.anchor, qi - off));  // catch-up eats literals only, stays in block
+    if (L == kFastLen && qi + kFastLen < b.mlim)   // long match: continue from memory
+      L += wave_count_fwd(b.src + uint32_t(qi + kFastLen), b.src + uint32_t(qi - off + kFastLen),
+                          b.mlim - qi - kFastLen, lane);
+    const int start = qi - bkq;
+    const uint32_t lit = uint32_t(start - b.anchor), ml = uint32_t(L + bkq);
+    if (lane == b.ns) {
+      b.seqA = lit | (ml << 16);
+      b.seqB = uint32_t(off);
+    }
+    b.anchor = b.p = start + int(ml);
+    if (++b.ns == 64 && !emit_batch(b, lane)) return false;
+  }
+  return true;
+}
+
+// one pipelined step: the lookup + gather of round R+64 and the window of
+// round R+192 are in flight while round R is measured and parsed (the window
+// of round R+64 was issued two steps earlier).  Every load is issued
+// unconditionally (parked lanes read nothing), so the vmcnt waits stay exact.
+__device__ __forceinline__ bool round_step(BlockCtx &b, Round &cu, Round &nx, int R,
+                                           lds_u16 *table, int lane) {
+  round_lookup(b, nx, R + 64, table, lane);
+  if (!round_parse(b, cu, R, lane)) return false;
+  round_load(b, cu, R + 192, lane);
+  return true;
+}
+
+// Compress one block of n (>= 13) bytes at src into dst (capacity n-1).
+// Returns the compressed size, or 0 when it does not fit (stored raw).
+__device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, int lane) {
+  BlockCtx b;
+  b.src = src;
+  b.dst = dst;
+  const uintptr_t lo = src & ~uintptr_t(3);
+  b.r = block_rsrc(lo, (src + uint32_t(n) + 3u) & ~uintptr_t(3));
+  b.sa = uint32_t(src & 3u);
+  b.n = n;
+  b.mfl = n - kLz4MFLimit;        // last position a match may start (lz4.c:907)
+  b.mlim = n - kLz4LastLiterals;  // matchlimit (lz4.c:822)
+  b.olimit = n - 1;               // LZ4F_makeBlock dstCapacity
+  b.anchor = b.p = b.op = b.ns = b.batch_anchor = 0;
+  b.seqA = b.seqB = 0;
+
+  Round A, B, C;
+  round_load(b, A, 0, lane);
+  round_load(b, B, 64, lane);
+  round_load(b, C, 128, lane);
+  round_lookup(b, A, 0, table, lane);
+  for (int R = 0; R <= b.mfl; R += 192) {
+    if (!round_step(b, A, B, R, table, lane)) return 0;
+    if (R + 64 > b.mfl) break;
+    if (!round_step(b, B, C, R + 64, table, lane)) return 0;
+    if (R + 128 > b.mfl) break;
+    if (!round_step(b, C, A, R + 128, table, lane)) return 0;
+  }
+  if (b.ns && !emit_batch(b, lane)) return 0;
+  // last literals (lz4.c:1141-1166)
+  const uint32_t last = uint32_t(n - b.anchor);
+  if (b.op + 1 + int(ext_bytes(last)) + int(last) > b.olimit) return 0;
+  if (lane == 0) {
+    uintptr_t p0 = dst + uint32_t(b.op);
+    stb(p0++, (last < 15u ? last : 15u) << 4);
+    if (last >= 15u) put_len(p0, last);
+  }
+  const int op = b.op + 1 + int(ext_bytes(last));
+  wave_copy_bytes(dst + uint32_t(op), src + uint32_t(b.anchor), last, lane);
+  return op + int(last);
+}
+
+__global__ __launch_bounds__(64) void lz4_fast_blocks_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
+    const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
+    const uint64_t *__restrict__ out_offs, uint32_t n) {
+  __shared__ __attribute__((aligned(16))) uint16_t table_mem[1u << kFastHashLog];
+  lds_u16 *table = (lds_u16 *)table_mem;
+  const int lane = threadIdx.x;
+  const uint64_t items = uint64_t(n) * kFastMaxItems;
+  for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const uint32_t f = uint32_t(it / kFastMaxItems), kk = uint32_t(it % kFastMaxItems);
+    const uint32_t len = uni(in_lens[f]);
+    const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
+    for (uint32_t k = kk; k < nb; k += kFastMaxItems) {
+      const uint32_t bn = (len - k * kLz4Block) < kLz4Block ? (len - k * kLz4Block) : kLz4Block;
+      const uintptr_t src = reinterpret_cast<uintptr_t>(in) + in_offs[f] + uint64_t(k) * kLz4Block;
+      const uintptr_t slot = reinterpret_cast<uintptr_t>(out) + out_offs[f] + 7u + uint64_t(k) * kFastSlot;
+      int csize = 0;
+      if (bn >= uint32_t(kLz4MFLimit + 1)) {
+        typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) u32x4e lds_u4;
+        lds_u4 *t4 = (lds_u4 *)table_mem;
+        const u32x4e z = {0u, 0u, 0u, 0u};
+        for (int x = lane; x < int((2u << kFastHashLog) / 16u); x += 64) t4[x] = z;
+        asm volatile("" ::: "memory");
+        csize = fast_block(src, int(bn), slot + 4u, table, lane);
+      }
+      if (lane == 0) {
+        const uint32_t w = csize ? uint32_t(csize) : (bn | 0x80000000u);  // LZ4F_makeBlock
+        stb(slot, w & 0xFFu); stb(slot + 1, (w >> 8) & 0xFFu);
+        stb(slot + 2, (w >> 16) & 0xFFu); stb(slot + 3, w >> 24);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
+                              const uint32_t *d_in_lens, uint8_t *d_out,
+                              const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
+                              hipStream_t s) {
+  if (!n) return 0;
+  const uint64_t items = uint64_t(n) * kFastMaxItems;
+  const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
+  hipLaunchKernelGGL(lz4_fast_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
+                     d_in_lens, d_out, d_out_offs, n);
+  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s);
+  RDK_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace rdk

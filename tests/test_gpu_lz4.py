@@ -239,3 +239,86 @@ def test_batch_scale_roundtrip_property(engine):
     assert bool(torch.equal(d_dec[:n * size], d_in[:n * size]))
     ol = out_lens.cpu().numpy()
     assert len(set(ol[i] for i in range(4))) >= 1 and all(ol[i] == ol[i % 4] for i in range(n))
+
+
+# ------------------------------------------------ throughput-mode compressor
+def _fast_compress(engine, inputs):
+    import torch
+    hbuf, hoffs = _pack(inputs)
+    d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
+    in_offs = torch.tensor(hoffs, dtype=torch.int64, device="cuda")
+    in_lens = torch.tensor([len(b) for b in inputs], dtype=torch.int32, device="cuda")
+    bounds = [engine.lz4f_compress_bound(len(b)) for b in inputs]
+    ooffs = np.concatenate([[0], np.cumsum([(b + 63) // 64 * 64 for b in bounds])[:-1]])
+    d_out = torch.empty(int(sum((b + 63) // 64 * 64 for b in bounds)) + 256, dtype=torch.uint8,
+                        device="cuda")
+    out_offs = torch.tensor(ooffs, dtype=torch.int64, device="cuda")
+    out_lens = torch.zeros(len(inputs), dtype=torch.int32, device="cuda")
+    engine.lz4f_compress_fast_batch(d_in, in_offs, in_lens, d_out, out_offs, out_lens)
+    host_out = bytes(d_out.cpu().numpy())
+    flens = out_lens.cpu().numpy()
+    return [host_out[ooffs[i]:ooffs[i] + flens[i]] for i in range(len(inputs))]
+
+
+def _fast_inputs(seed, count):
+    rnd = random.Random(seed)
+    sizes = [0, 1, 12, 13, 14, 100, 4095, 65535, 65536, 65537, 1000000, 1 << 20] + \
+            [rnd.randrange(1, 300000) for _ in range(count)]
+    out = []
+    for i, n in enumerate(sizes):
+        kind = i % 5
+        if kind == 0:
+            out.append(W.gen_json(n, i))
+        elif kind == 1:
+            out.append(rnd.randbytes(n))
+        elif kind == 2:
+            out.append(bytes(n))
+        elif kind == 3:
+            base = rnd.randbytes(max(1, n // 50))
+            out.append((base * 60)[:n])
+        else:
+            words = [rnd.randbytes(rnd.randrange(2, 9)) for _ in range(200)]
+            out.append(b" ".join(rnd.choice(words) for _ in range(n // 4 + 1))[:n])
+    return out
+
+
+def test_fast_compress_decodes_with_reference(engine, oracle_mod):
+    """Every throughput-mode frame decodes to its input with the reference's
+    own decoder (oracle/_ref build of lz4frame.c via rd_kafka_lz4_decompress's
+    loop when present here; the pinned restatement on the GPU box) and with
+    the GPU decoder; frame structure is the reference's (header, 64 KiB
+    independent blocks, raw fallback, end mark)."""
+    inputs = _fast_inputs(41, 30)
+    frames = _fast_compress(engine, inputs)
+    use_ref = oracle_mod.ref_available()
+    for i, (b, fr) in enumerate(zip(inputs, frames)):
+        assert fr[:7] == bytes([0x04, 0x22, 0x4D, 0x18, 0x60, 0x40, 0x82]), i
+        assert fr[-4:] == b"\0\0\0\0", i
+        e, out = oracle_mod.ref_rdk_lz4_decompress(fr, max_msg_size=1 << 30)[:2] if use_ref \
+            else oracle_mod.rdk_lz4_decompress(fr)
+        assert e == 0 and out == b, (i, len(b), e)
+        e2, out2 = engine.rd_kafka_lz4_decompress(1, 0, fr)
+        assert e2 == 0 and out2 == b, i
+        # every block is no larger than the reference's worst case (raw + 4)
+        assert len(fr) <= engine.lz4f_compress_bound(len(b)), i
+
+
+def test_fast_compress_ratio_within_5pct(engine, oracle_mod):
+    """north_star: compression ratio within 5 % of the reference's CPU lz4 on
+    the same input (JSON records of configs[2], text-like and repetitive)."""
+    rnd = random.Random(43)
+    words = [bytes(rnd.choice(b"abcdefghij") for _ in range(rnd.randrange(2, 10)))
+             for _ in range(500)]
+    text = b" ".join(rnd.choice(words) for _ in range(300000))[:1 << 20]
+    inputs = [W.gen_json(1 << 20, 42), W.gen_json(65536, 7), W.gen_json(1 << 20, 5), text,
+              (rnd.randbytes(3000) * 400)[:1 << 20]]
+    frames = _fast_compress(engine, inputs)
+    for i, (b, fr) in enumerate(zip(inputs, frames)):
+        ref = oracle_mod.rdk_lz4_compress(b)[1]
+        r_gpu, r_ref = len(b) / len(fr), len(b) / len(ref)
+        assert r_gpu >= 0.95 * r_ref, (i, r_gpu, r_ref)
+
+
+def test_fast_compress_deterministic(engine):
+    inputs = _fast_inputs(44, 8)
+    assert _fast_compress(engine, inputs) == _fast_compress(engine, inputs)

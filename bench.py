@@ -414,6 +414,8 @@ def main():
             line["legs"] = {
                 "lz4f_compress_1MiB_json": leg_line("lz4c", bench_lz4c(sub, rank, world), 3, 1,
                                                     cpu("compress")),
+                "lz4f_compress_fast_1MiB_json": leg_line(
+                    "lz4c_fast", bench_lz4c(sub, rank, world, fast=True), 3, 1, cpu("compress")),
                 "consumer_crc_verify_lz4f_decompress_1MiB": leg_line(
                     "consumer", bench_consumer(sub, rank, world), 3, 1, cpu("decompress")),
             }

@@ -43,7 +43,7 @@ namespace {
 
 constexpr int kFastMaxItems = 64;              // block slots per frame per pass
 constexpr uint32_t kFastSlot = kLz4Block + 4;  // worst-case bytes per block in a frame
-constexpr uint32_t kFastHashLog = 13;
+constexpr uint32_t kFastHashLog = 12;
 constexpr int kFastLen = 28;                   // match bytes measured from registers
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
@@ -89,15 +89,18 @@ __device__ __forceinline__ void load5(rsrc_t r, uint32_t a, uint32_t d[5]) {
   d[4] = __builtin_amdgcn_raw_buffer_load_b32(r, a + 16u, 0, 0);
 }
 
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_t &total) {
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(x, d);
-    if (lane >= d) x += t;
-  }
-  total = __builtin_amdgcn_readlane(x, 63);
-  return x - v;
+// exclusive prefix sum over the wave by DPP row shifts and row broadcasts
+// (no LDS round trips); `total` gets the wave sum
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t &total) {
+  int x = int(v);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false); // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false); // row_bcast:31
+  total = uint32_t(__builtin_amdgcn_readlane(x, 63));
+  return uint32_t(x) - v;
 }
 
 // equal bytes a[i]==b[i] for i in [0, limit), 64 per wave step
@@ -148,35 +151,129 @@ struct BlockCtx {
   rsrc_t r;            // the block's dwords
   uint32_t sa;         // src & 3: byte offset of position 0 inside the resource
   int n, mfl, mlim, olimit;
-  int anchor, p, op, ns, batch_anchor;
-  uint32_t seqA, seqB; // lane j: sequence j of the current batch (lit | ml<<16, offset)
+  int p;               // parse position == anchor (end of the last match)
+  int op;              // output bytes written
 };
 
-// Emit the b.ns collected sequences at dst+op.  Returns false when the block
-// would not fit in olimit bytes (stored raw).
-__device__ bool emit_batch(BlockCtx &b, int lane) {
-  const bool on = lane < b.ns;
-  const uint32_t lit = on ? (b.seqA & 0xFFFFu) : 0u;
-  const uint32_t ml = on ? (b.seqA >> 16) : 0u;
-  const uint32_t sz = on ? 3u + lit + ext_bytes(lit) + ext_bytes(ml - 4u) : 0u;
-  uint32_t tot_sz, tot_span;
-  const uint32_t o = wave_excl_scan(sz, lane, tot_sz);
-  const uint32_t a = wave_excl_scan(lit + ml, lane, tot_span);
-  (void)tot_span;
+// Per round the lane's own 36-byte window (Win, loaded three rounds ahead),
+// and its candidate with the candidate's window (Cand, gathered one round
+// ahead).
+struct Win {
+  uint32_t d[9];
+};
+struct Cand {
+  uint32_t t[9];
+  int c;
+};
+
+__device__ __forceinline__ void round_load(const BlockCtx &b, Win &x, int R, int lane) {
+  const int i = R + lane;
+  load9(b.r, i <= b.mfl ? ((uint32_t(i) + b.sa) & ~3u) : kNoLoad, x.d);
+}
+
+// hash + table for the round at R (window x.d arrived), then issue the
+// candidate gather for the lanes the parse may still need (i >= p).  All 64
+// lanes store their position in one ds_write_b16; where several hit the same
+// entry the highest lane -- the latest position -- is the one that lands
+// (measured on gfx950; a fixed order either way, so the output is
+// deterministic).
+__device__ __forceinline__ void round_lookup(const BlockCtx &b, const Win &x, Cand &y, int R,
+                                             lds_u16 *table, int lane) {
+  const int i = R + lane;
+  const bool act = i <= b.mfl;
+  const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
+  const uint32_t h = hash4(__builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi));
+  const int c = act ? int(table[h]) : 0;
+  if (act) table[h] = uint16_t(i);
+  y.c = (act && i >= b.p && c < i) ? c : -1;
+  load9(b.r, y.c >= 0 ? ((uint32_t(c) + b.sa) & ~3u) : kNoLoad, y.t);
+}
+
+// Measure the round's matches (windows arrived), walk the greedy parse over
+// it (scalar: one ctz + one readlane per sequence), then emit the chosen
+// sequences together: every chosen lane writes its own token, literals,
+// offset and length bytes at a wave-prefix-sum position.  Returns false when
+// the block does not fit in olimit bytes (stored raw).
+__device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Cand &y, int R,
+                                            int lane) {
+  const int i = R + lane;
+  const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
+  const uint32_t shc = (uint32_t(y.c) + b.sa) & 3u;
+  const bool valid = y.c >= 0 && i >= b.p &&
+                     __builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi) ==
+                         __builtin_amdgcn_alignbyte(y.t[2], y.t[1], shc);
+  const uint64_t vm = ballot(valid);
+  if (!vm) return true;
+  int len = kFastLen;
+#pragma unroll
+  for (int k = 6; k >= 1; --k) {
+    const uint32_t z = __builtin_amdgcn_alignbyte(x.d[k + 2], x.d[k + 1], shi) ^
+                       __builtin_amdgcn_alignbyte(y.t[k + 2], y.t[k + 1], shc);
+    if (z) len = 4 * k + (__builtin_ctz(z) >> 3);
+  }
+  if (len > b.mlim - i) len = b.mlim - i;
+
+  // greedy walk: first verified position at or after the end of the last match
+  const int xin = b.p - R;
+  int xr = xin;
+  uint64_t chosen = 0;
+  for (;;) {
+    const int rel = xr > 0 ? xr : 0;
+    if (rel >= 64) break;
+    const uint64_t m = vm & (~0ull << rel);
+    if (!m) break;
+    const int q = __builtin_ctzll(m);
+    int L = __builtin_amdgcn_readlane(len, q);
+    if (L == kFastLen && R + q + kFastLen < b.mlim) {  // long match: continue from memory
+      const int qi = R + q, off = qi - __builtin_amdgcn_readlane(y.c, q);
+      L += wave_count_fwd(b.src + uint32_t(qi + kFastLen), b.src + uint32_t(qi - off + kFastLen),
+                          b.mlim - qi - kFastLen, lane);
+      if (lane == q) len = L;
+    }
+    chosen |= 1ull << q;
+    xr = q + L;
+  }
+  if (!chosen) return true;
+  b.p = R + xr;
+
+  // sequence fields of the chosen lanes
+  const bool ch = (chosen >> lane) & 1ull;
+  const uint64_t below = chosen & ((1ull << lane) - 1ull);
+  const int pl = below ? 63 - __builtin_clzll(below) : lane;
+  const int pend = __shfl(lane + len, pl);       // end of the previous chosen match
+  const int prev = below ? pend : xin;           // this sequence's anchor (relative)
+  const uint32_t xb = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi) ^
+                      __builtin_amdgcn_alignbyte(y.t[1], y.t[0], shc);
+  int bk = xb ? int(__builtin_clz(xb) >> 3) : 4;  // catch-up bytes (lz4.c:957)
+  bk = min(bk, min(lane - prev, y.c));            // literals only, inside the block
+  const uint32_t lit = ch ? uint32_t(lane - bk - prev) : 0u;
+  const uint32_t ml = uint32_t(len + bk);
+  const uint32_t sz = ch ? 3u + lit + ext_bytes(lit) + ext_bytes(ml - 4u) : 0u;
+  uint32_t tot;
+  const uint32_t o = wave_excl_scan(sz, tot);
   // keep room for the shortest possible last-literals token (lz4.c:1146)
-  if (b.op + int(tot_sz) + 1 > b.olimit) return false;
-  const uint32_t lstart = uint32_t(b.batch_anchor) + a;
-  // short literal runs come from one 20-byte window per lane (one load)
-  const uint32_t al = lstart + b.sa;
+  if (b.op + int(tot) + 1 > b.olimit) return false;
+  const uint32_t lstart = uint32_t(R + prev);    // absolute literal start
+  // literal bytes: up to 4 (with the catch-up) sit in the lane's own back
+  // dword; longer short runs come from a 20-byte window
+  const bool in_reg = lit + uint32_t(bk) <= 4u;
+  const bool need_win = ch && !in_reg && lit <= kShortLit;
   uint32_t w[5];
-  load5(b.r, (on && lit && lit <= kShortLit) ? (al & ~3u) : kNoLoad, w);
-  if (on) {
+  if (ballot(need_win)) load5(b.r, need_win ? ((lstart + b.sa) & ~3u) : kNoLoad, w);
+  if (ch) {
     uintptr_t p = b.dst + uint32_t(b.op) + o;
     const uint32_t mc = ml - 4u;
     stb(p++, ((lit < 15u ? lit : 15u) << 4) | (mc < 15u ? mc : 15u));
     if (lit >= 15u) p = put_len(p, lit);
-    if (lit <= kShortLit) {
-      const uint32_t sh = al & 3u;
+    if (in_reg) {
+      // bytes i-4..i-1 of the lane's window; the literals end bk before i
+      const uint32_t back = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi);
+      const uint32_t first = 4u - uint32_t(bk) - lit;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k)
+        if (k < lit) stb(p + k, back >> (8u * (first + k)));
+    } else if (lit <= kShortLit) {
+      const uint32_t sh = (lstart + b.sa) & 3u;
       uint32_t v[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
@@ -185,13 +282,14 @@ __device__ bool emit_batch(BlockCtx &b, int lane) {
         if (k < lit) stb(p + k, v[k >> 2] >> (8u * (k & 3u)));
     }
     p += lit;
-    stb(p, b.seqB & 0xFFu);
-    stb(p + 1, (b.seqB >> 8) & 0xFFu);
+    const uint32_t off = uint32_t(i - y.c);
+    stb(p, off & 0xFFu);
+    stb(p + 1, off >> 8);
     p += 2;
     if (mc >= 15u) put_len(p, mc);
   }
   // long literal runs: the whole wave copies them one at a time
-  uint64_t longm = ballot(on && lit > kShortLit);
+  uint64_t longm = ballot(ch && lit > kShortLit);
   while (longm) {
     const int j = __builtin_ctzll(longm);
     longm &= longm - 1;
@@ -200,109 +298,21 @@ __device__ bool emit_batch(BlockCtx &b, int lane) {
     const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
     wave_copy_bytes(b.dst + uint32_t(b.op) + jo + 1u + ext_bytes(jl), b.src + js, jl, lane);
   }
-  b.op += int(tot_sz);
-  b.ns = 0;
-  b.batch_anchor = b.anchor;
+  b.op += int(tot);
   return true;
 }
 
-// One round of 64 positions in flight: the lane's own 40-byte window, its
-// candidate (or -1) and the candidate's window.
-struct Round {
-  uint32_t d[9];
-  uint32_t t[9];
-  int c;
-};
-
-__device__ __forceinline__ void round_load(const BlockCtx &b, Round &x, int R, int lane) {
-  const int i = R + lane;
-  load9(b.r, i <= b.mfl ? ((uint32_t(i) + b.sa) & ~3u) : kNoLoad, x.d);
-}
-
-// hash + table for the round at R (window x.d arrived), then issue the
-// candidate gather for the lanes the parse may still need (i >= p)
-__device__ __forceinline__ void round_lookup(const BlockCtx &b, Round &x, int R, lds_u16 *table,
-                                             int lane) {
-  const int i = R + lane;
-  const bool act = i <= b.mfl;
-  const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
-  const uint32_t s0 = __builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi);
-  const uint32_t h = hash4(s0);
-  const int c = act ? int(table[h]) : 0;
-  // insert position i; the largest position of a hash wins (deterministic)
-  if (act) table[h] = uint16_t(i);
-  for (;;) {
-    const bool fix = act && int(table[h]) < i;
-    if (!ballot(fix)) break;
-    if (fix) table[h] = uint16_t(i);
-  }
-  x.c = (act && i >= b.p && c < i) ? c : -1;
-  load9(b.r, x.c >= 0 ? ((uint32_t(c) + b.sa) & ~3u) : kNoLoad, x.t);
-}
-
-// measure the round's matches (windows arrived), then parse it greedily
-__device__ __forceinline__ bool round_parse(BlockCtx &b, const Round &x, int R, int lane) {
-  const int i = R + lane;
-  const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
-  const uint32_t shc = (uint32_t(x.c) + b.sa) & 3u;
-  const bool valid = x.c >= 0 && i >= b.p &&
-                     __builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi) ==
-                         __builtin_amdgcn_alignbyte(x.t[2], x.t[1], shc);
-  int len = kFastLen;
-#pragma unroll
-  for (int k = 6; k >= 1; --k) {
-    const uint32_t y = __builtin_amdgcn_alignbyte(x.d[k + 2], x.d[k + 1], shi) ^
-                       __builtin_amdgcn_alignbyte(x.t[k + 2], x.t[k + 1], shc);
-    if (y) len = 4 * k + (__builtin_ctz(y) >> 3);
-  }
-  if (len > b.mlim - i) len = b.mlim - i;
-  const uint32_t xb = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi) ^
-                      __builtin_amdgcn_alignbyte(x.t[1], x.t[0], shc);
-  const uint32_t bk = xb ? uint32_t(__builtin_clz(xb) >> 3) : 4u;
-  const uint32_t pack = uint32_t(len) | (bk << 6) | (uint32_t(i - x.c) << 9);
-  const uint64_t vm = ballot(valid);
-#ifdef RDK_FAST_DEBUG
-  if (R == 0 && lane < 4)
-    printf("lane %d c %d valid %d shi %u shc %u d %08x %08x %08x t %08x %08x %08x len %d\n", lane,
-           x.c, int(valid), shi, shc, x.d[0], x.d[1], x.d[2], x.t[0], x.t[1], x.t[2], len);
-#endif
-  for (;;) {
-    const int rel = b.p - R;
-    if (rel >= 64) break;
-    const uint64_t m = rel > 0 ? (vm & (~0ull << rel)) : vm;
-    if (!m) break;
-    const int q = __builtin_ctzll(m);
-    const uint32_t pk = __builtin_amdgcn_readlane(pack, q);
-    const int qi = R + q;
-    const int off = int(pk >> 9);
-    int L = int(pk & 63u);
-    int bkq = int((pk >> 6) & 7u);
-    bkq = min(bkq, min(qi - b.anchor, qi - off));  // catch-up eats literals only, stays in block
-    if (L == kFastLen && qi + kFastLen < b.mlim)   // long match: continue from memory
-      L += wave_count_fwd(b.src + uint32_t(qi + kFastLen), b.src + uint32_t(qi - off + kFastLen),
-                          b.mlim - qi - kFastLen, lane);
-    const int start = qi - bkq;
-    const uint32_t lit = uint32_t(start - b.anchor), ml = uint32_t(L + bkq);
-    if (lane == b.ns) {
-      b.seqA = lit | (ml << 16);
-      b.seqB = uint32_t(off);
-    }
-    b.anchor = b.p = start + int(ml);
-    if (++b.ns == 64 && !emit_batch(b, lane)) return false;
-  }
-  return true;
-}
-
-// one pipelined step: the lookup + gather of round R+64 and the window of
-// round R+192 are in flight while round R is measured and parsed (the window
-// of round R+64 was issued two steps earlier).  Every load is issued
-// unconditionally (parked lanes read nothing), so the vmcnt waits stay exact.
-__device__ __forceinline__ bool round_step(BlockCtx &b, Round &cu, Round &nx, int R,
-                                           lds_u16 *table, int lane) {
-  round_lookup(b, nx, R + 64, table, lane);
-  if (!round_parse(b, cu, R, lane)) return false;
-  round_load(b, cu, R + 192, lane);
-  return true;
+// One pipelined step: the lookup + gather of round R+64 and the window of
+// round R+192 are issued before round R is measured and parsed, so the
+// stores of the previous round's emission never sit between a load and its
+// first use (vmcnt counts loads and stores together).  Every load is issued
+// unconditionally (parked lanes read nothing), so the waits stay exact.
+__device__ __forceinline__ bool round_step(BlockCtx &b, const Win &cur, Win &next, Win &far,
+                                           const Cand &ccur, Cand &cnext, int R, lds_u16 *table,
+                                           int lane) {
+  round_lookup(b, next, cnext, R + 64, table, lane);
+  round_load(b, far, R + 192, lane);
+  return round_parse(b, cur, ccur, R, lane);
 }
 
 // Compress one block of n (>= 13) bytes at src into dst (capacity n-1).
@@ -318,24 +328,25 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
   b.mfl = n - kLz4MFLimit;        // last position a match may start (lz4.c:907)
   b.mlim = n - kLz4LastLiterals;  // matchlimit (lz4.c:822)
   b.olimit = n - 1;               // LZ4F_makeBlock dstCapacity
-  b.anchor = b.p = b.op = b.ns = b.batch_anchor = 0;
-  b.seqA = b.seqB = 0;
+  b.p = b.op = 0;
 
-  Round A, B, C;
-  round_load(b, A, 0, lane);
-  round_load(b, B, 64, lane);
-  round_load(b, C, 128, lane);
-  round_lookup(b, A, 0, table, lane);
-  for (int R = 0; R <= b.mfl; R += 192) {
-    if (!round_step(b, A, B, R, table, lane)) return 0;
+  Win W0, W1, W2, W3;
+  Cand C0, C1;
+  round_load(b, W0, 0, lane);
+  round_load(b, W1, 64, lane);
+  round_load(b, W2, 128, lane);
+  round_lookup(b, W0, C0, 0, table, lane);
+  for (int R = 0; R <= b.mfl; R += 256) {
+    if (!round_step(b, W0, W1, W3, C0, C1, R, table, lane)) return 0;
     if (R + 64 > b.mfl) break;
-    if (!round_step(b, B, C, R + 64, table, lane)) return 0;
+    if (!round_step(b, W1, W2, W0, C1, C0, R + 64, table, lane)) return 0;
     if (R + 128 > b.mfl) break;
-    if (!round_step(b, C, A, R + 128, table, lane)) return 0;
+    if (!round_step(b, W2, W3, W1, C0, C1, R + 128, table, lane)) return 0;
+    if (R + 192 > b.mfl) break;
+    if (!round_step(b, W3, W0, W2, C1, C0, R + 192, table, lane)) return 0;
   }
-  if (b.ns && !emit_batch(b, lane)) return 0;
   // last literals (lz4.c:1141-1166)
-  const uint32_t last = uint32_t(n - b.anchor);
+  const uint32_t last = uint32_t(n - b.p);
   if (b.op + 1 + int(ext_bytes(last)) + int(last) > b.olimit) return 0;
   if (lane == 0) {
     uintptr_t p0 = dst + uint32_t(b.op);
@@ -343,7 +354,7 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
     if (last >= 15u) put_len(p0, last);
   }
   const int op = b.op + 1 + int(ext_bytes(last));
-  wave_copy_bytes(dst + uint32_t(op), src + uint32_t(b.anchor), last, lane);
+  wave_copy_bytes(dst + uint32_t(op), src + uint32_t(b.p), last, lane);
   return op + int(last);
 }
 

@@ -398,6 +398,8 @@ safe_decode:
   return op;
 }
 
+#include "lz4_decode_fast.h"
+
 // ------------------------------------------------------------ kernels
 struct DevReader {
   uintptr_t p;
@@ -450,6 +452,13 @@ __device__ int run_block(const BlockInfo &b, uintptr_t frame, uintptr_t dst, uin
   if (b.flags & B_XXH) {
     uint32_t h = lane == 0 ? xxh32_lane(src, b.csize, 0) : 0u;
     if (uni(h) != b.xxh) return -1;
+  }
+  if (hist == 0 && !(b.flags & B_TRUNC) && realcap >= 0) {
+    const int r = decode_block_fast(src, b.csize, dst, max_block, uint32_t(realcap), ring, lane);
+    if (r != kFastFallback) return r;
+#ifdef RDK_DEC_DEBUG
+    if (lane == 0) printf("fallback src_off %u csize %u\n", b.src_off, b.csize);
+#endif
   }
   OutRing o{dst, ring, 0u};
   return decode_block(src, int(b.csize), o, int(max_block), realcap, hist, lane);

@@ -1,0 +1,315 @@
+// lz4_decode_fast.h -- batched LZ4 block decoder (independent blocks).
+//
+// Included by lz4_decode.hip.  decode_block_fast() decodes one independent
+// block (LZ4_decompress_safe_usingDict with noDict, lz4.c:2307 ->
+// LZ4_decompress_generic lz4.c:1654-2068) without the per-sequence wave
+// round trips of the exact decoder:
+//
+//   1. DISCOVERY: the compressed block is cut into fixed 64-byte segments.
+//      For every byte position p of a segment, lane p%64 parses the
+//      sequence that WOULD start at p (token, literal / match length bytes,
+//      offset) from a 24-byte register window of its own, so a whole
+//      segment's candidates cost two loads and ~40 VALU.
+//   2. WALK: the true sequence chain is followed with one v_readlane per
+//      sequence (next start -> lane), scalar.  Each sequence "paints" the
+//      64-byte output chunk under construction: lane l of the chunk records
+//      where output byte oc+l comes from (an input position for literals,
+//      an earlier output position for matches).
+//   3. FLUSH: a complete chunk resolves its in-chunk match sources by
+//      pointer jumping (ds_bpermute, only when some offset < 64), fetches
+//      every byte at once (input, the wave's 8 KiB LDS history ring, or the
+//      already written output in HBM) and stores 64 contiguous bytes.
+//
+// The fast path only returns a result when the block is PROVABLY accepted
+// by the reference with this output: every condition under which
+// LZ4_decompress_generic would return an error (or could even take a
+// different branch that matters) is checked -- offset 0, a match before the
+// block start, length bytes read too close to the input end (lz4.c:1625
+// read_variable_length limits), the end-of-block literal / match margins
+// (MFLIMIT, LASTLITERALS, lz4.c:1850-1880 / 1986-2004), the last sequence
+// ending exactly at the input end, the caller's capacity.  Anything else
+// returns kFastFallback and the block is re-decoded from scratch by the
+// exact decoder (decode_block), which then decides the verdict.
+// (textually included inside namespace rdk, after the ring definitions)
+#pragma once
+
+constexpr int kFastFallback = -100;
+constexpr uint32_t kLitTag = 0x80000000u;
+constexpr uint32_t kSeqComplex = 0xFFFFFFFFu;  // header longer than the lane window
+constexpr uint32_t kSeqBad = 0xFFFFFFFEu;      // the reference would reject it
+constexpr uint32_t kNoAccess = 0x80000000u;    // out-of-range buffer offset (reads 0)
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(uintptr_t base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), 0, int(bytes),
+                                           0x00020000);
+}
+
+struct FastDec {
+  uintptr_t dst;
+  lds_u8 *ring;      // kRing bytes of the newest output
+  rsrc_t rin;        // compressed block [0, csize)
+  rsrc_t rout;       // block output [0, realcap)
+  uint32_t csize, oend, realcap;
+  uint32_t oc;       // output position of the chunk being painted
+  uint32_t dsrc;     // lane l: source of output byte oc+l (kLitTag | input pos, or output pos)
+};
+
+// Resolve, fetch and store output bytes [oc, oc+nvalid) of the painted chunk.
+__device__ __forceinline__ void fast_flush(FastDec &d, uint32_t nvalid, int lane) {
+  uint32_t src = d.dsrc;
+  const bool live = uint32_t(lane) < nvalid;
+  // match sources inside this chunk: pointer jumping, each step halves the
+  // remaining hops (sources always point to lower lanes)
+  for (;;) {
+    const bool intra = live && !(src & kLitTag) && src >= d.oc;
+    if (!ballot(intra)) break;
+    const uint32_t v = uint32_t(__shfl(int(src), intra ? int(src - d.oc) : lane));
+    if (intra) src = v;
+  }
+  const bool lit = (src & kLitTag) != 0u;
+  const uint32_t q = src & ~kLitTag;
+  const bool ring_ok = !lit && q + kRing >= d.oc;  // still in the history ring
+  const bool far = live && !lit && !ring_ok;
+  // far history was stored >= kRing/64 chunks (>= 64 vector-memory ops) ago:
+  // with in-order vmcnt retirement it has completed, so no wait is needed
+  const uint32_t lb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live && lit) ? q : kNoAccess, 0, 0);
+  const uint32_t fb = __builtin_amdgcn_raw_buffer_load_b8(d.rout, far ? q : kNoAccess, 0, 0);
+  const uint32_t rb = d.ring[q & kRingMask] & (ring_ok ? 0xFFu : 0u);
+  // each lane's byte arrives in exactly one of the three (parked loads read 0)
+  const uint32_t v = lb | fb | rb;
+  if (live) d.ring[(d.oc + uint32_t(lane)) & kRingMask] = uint8_t(v);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), d.rout, live ? d.oc + uint32_t(lane) : kNoAccess,
+                                      0, 0);
+}
+
+// output [a, b) takes its bytes from source positions s, s+1, ... (tag marks
+// input positions); completes and flushes chunks on the way
+__device__ __forceinline__ void fast_paint(FastDec &d, uint32_t a, uint32_t b, uint32_t s,
+                                           uint32_t tag, int lane) {
+  while (a < b) {
+    const uint32_t ce = d.oc + 64u;
+    const uint32_t e = b < ce ? b : ce;
+    const uint32_t rel = uint32_t(lane) + d.oc - a;
+    if (rel < e - a) d.dsrc = (s + rel) | tag;
+    s += e - a;
+    a = e;
+    if (a == ce) {
+      fast_flush(d, 64u, lane);
+      d.oc = ce;
+    }
+  }
+}
+
+// Candidate sequence of lane `lane` of segment [seg, seg+64): the sequence
+// that would start at p = seg+lane, parsed from 24 bytes of registers.
+//   A: next sequence start, kSeqComplex, or kSeqBad
+//   B: literal length | match length << 16 (match length 0: last sequence)
+//   C: offset | (literal start - p) << 16
+struct SegCand {
+  uint32_t A, B, C;
+};
+
+// 20 bytes of a lane's window as named words (no array: a runtime-indexed
+// register array would be demoted to scratch)
+struct Win20 {
+  uint32_t w0, w1, w2, w3, w4;
+};
+
+// 4 bytes starting `k` bytes into the window (k <= 19; bytes past 20 read 0)
+__device__ __forceinline__ uint32_t win4(const Win20 &w, uint32_t k) {
+  const uint32_t j = k >> 2;
+  const uint32_t lo = j == 0 ? w.w0 : j == 1 ? w.w1 : j == 2 ? w.w2 : j == 3 ? w.w3 : w.w4;
+  const uint32_t hi = j == 0 ? w.w1 : j == 1 ? w.w2 : j == 2 ? w.w3 : j == 3 ? w.w4 : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, k & 3u);
+}
+
+__device__ __forceinline__ SegCand seg_parse(const FastDec &d, uint32_t seg, int lane) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  const uint32_t p = seg + uint32_t(lane);
+  const uint32_t a = p & ~3u, sh = p & 3u;
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(d.rin, a, 0, 0);
+  const u2 x = __builtin_amdgcn_raw_buffer_load_b64(d.rin, a + 16u, 0, 0);
+  Win20 w;  // bytes p .. p+19
+  w.w0 = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
+  w.w1 = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
+  w.w2 = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
+  w.w3 = __builtin_amdgcn_alignbyte(x.x, v.w, sh);
+  w.w4 = __builtin_amdgcn_alignbyte(x.y, x.x, sh);
+  const uint32_t csize = d.csize;
+  SegCand c;
+  const uint32_t tok = w.w0 & 0xFFu;
+  uint32_t ll = tok >> 4, k = 1u;
+  bool complex = false, bad = false;
+  if (ll == 15u) {
+    // read_variable_length(iend-15, initial_check): error if ip >= iend-15
+    if (p + 1u >= csize - 15u || csize < 16u) bad = true;
+    uint32_t b;
+    do {
+      b = (win4(w, k) & 0xFFu);
+      // a 255 read at ip >= iend-15 stops the reference's loop early
+      // (loop_error, tolerated for literals) where this parse would go on
+      if (b == 255u && p + k + 1u >= csize - 15u) bad = true;
+      ll += b;
+      ++k;
+    } while (b == 255u && k < 4u);
+    if (b == 255u) complex = true;  // run continues past the window
+  }
+  const uint32_t lit_end = p + k + ll;
+  uint32_t ml = 0, off = 0, next;
+  if (lit_end == csize) {  // literals-only last sequence
+    next = csize;
+  } else {
+    const uint32_t r = lit_end - p;
+    if (r + 3u > 20u) {
+      complex = true;
+      next = 0;
+    } else {
+      const uint32_t dw = win4(w, r);
+      off = dw & 0xFFFFu;
+      if (off == 0u) bad = true;  // the reference writes garbage for it
+      ml = tok & 15u;
+      uint32_t m = r + 2u;
+      if (ml == 15u) {
+        uint32_t b;
+        do {
+          if (m >= 20u) { complex = true; break; }
+          b = win4(w, m) & 0xFFu;
+          // read_variable_length(iend-LASTLITERALS+1): error once ip >= iend-4
+          if (p + m + 1u >= csize - 4u || csize < 5u) bad = true;
+          ml += b;
+          ++m;
+        } while (b == 255u);
+      }
+      ml += uint32_t(kLz4MinMatch);
+      next = p + m;
+    }
+  }
+  c.A = bad ? kSeqBad : (complex ? kSeqComplex : next);
+  c.B = (ll & 0xFFFFu) | (ml << 16);
+  c.C = off | (k << 16);
+  if (p >= csize) c.A = kSeqBad;  // no sequence can start past the input
+  return c;
+}
+
+// Byte `i` of the compressed block, wave-uniform (slow path only).
+__device__ __forceinline__ uint32_t in_byte(rsrc_t rin, uint32_t i) {
+  return __builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b8(rin, i, 0, 0));
+}
+
+// Scalar parse of the sequence at p whose header does not fit a lane
+// window (long literal / match length runs).  Same checks as seg_parse.
+__device__ __forceinline__ SegCand seq_slow(rsrc_t rin, uint32_t csize, uint32_t p) {
+  SegCand c;
+  uint32_t tok = in_byte(rin, p), ll = tok >> 4, k = 1u;
+  bool bad = false;
+  if (ll == 15u) {
+    if (p + 1u >= csize - 15u || csize < 16u) bad = true;
+    uint32_t b;
+    do {
+      if (p + k >= csize) { bad = true; break; }
+      b = in_byte(rin, p + k);
+      if (b == 255u && p + k + 1u >= csize - 15u) bad = true;
+      ll += b;
+      ++k;
+    } while (b == 255u);
+  }
+  const uint32_t lit_end = p + k + ll;
+  uint32_t ml = 0, off = 0, next = csize;
+  if (!bad && lit_end != csize) {
+    if (lit_end + 2u > csize) bad = true;
+    else {
+      off = in_byte(rin, lit_end) | (in_byte(rin, lit_end + 1u) << 8);
+      if (off == 0u) bad = true;
+      ml = tok & 15u;
+      uint32_t m = lit_end + 2u;
+      if (ml == 15u) {
+        uint32_t b;
+        do {
+          if (m >= csize || m + 1u >= csize - 4u || csize < 5u) { bad = true; break; }
+          b = in_byte(rin, m);
+          ml += b;
+          ++m;
+        } while (b == 255u);
+      }
+      ml += uint32_t(kLz4MinMatch);
+      next = m;
+    }
+  }
+  if (ll > 0xFFFFu || ml > 0xFFFFu) bad = true;
+  c.A = bad ? kSeqBad : next;
+  c.B = (ll & 0xFFFFu) | (ml << 16);
+  c.C = off | (k << 16);
+  return c;
+}
+
+// Decode one independent block.  Returns the decoded size or kFastFallback.
+__device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, uint32_t oend,
+                                 uint32_t realcap, lds_u8 *ring, int lane) {
+  if (csize < 16u || csize > 65536u || oend > 65536u || oend < 64u) return kFastFallback;
+  FastDec d;
+  d.dst = dst;
+  d.ring = ring;
+  d.rin = make_rsrc(src, csize);
+  d.rout = make_rsrc(dst, realcap);
+  d.csize = csize;
+  d.oend = oend;
+  d.realcap = realcap;
+  d.oc = 0;
+  d.dsrc = 0;
+
+  uint32_t op = 0, ip = 0;
+  // the last non-final sequence decides the end-of-block margins
+  uint32_t last_cpy = 0, last_lit_end = 0, last_mend = 0;
+  uint32_t seg = 0;
+  SegCand cur = seg_parse(d, 0u, lane);
+  SegCand nxt = seg_parse(d, 64u, lane);
+  for (;;) {
+    // walk the chain through segment [seg, seg+64)
+    while (ip < seg + 64u) {
+      const uint32_t x = ip - seg;
+      uint32_t A = __builtin_amdgcn_readlane(cur.A, x);
+      uint32_t B, C;
+      if (A == kSeqComplex) {
+        const SegCand s = seq_slow(d.rin, d.csize, ip);
+        A = s.A; B = s.B; C = s.C;
+      } else {
+        B = __builtin_amdgcn_readlane(cur.B, x);
+        C = __builtin_amdgcn_readlane(cur.C, x);
+      }
+      if (A == kSeqBad) return kFastFallback;
+      const uint32_t ll = B & 0xFFFFu, ml = B >> 16, off = C & 0xFFFFu;
+      const uint32_t ls = ip + (C >> 16);
+      const uint32_t cpy = op + ll;
+      if (cpy + ml > realcap) return kFastFallback;  // the exact path reports the size error
+      fast_paint(d, op, cpy, ls, kLitTag, lane);
+      if (ml == 0u) {  // last sequence: literals end exactly at the input end
+        if (ls + ll != csize || cpy > oend) return kFastFallback;
+        if (op && (last_cpy > oend - uint32_t(kLz4MFLimit) ||
+                   last_lit_end > csize - uint32_t(2 + 1 + kLz4LastLiterals) ||
+                   last_mend > oend - uint32_t(kLz4LastLiterals)))
+          return kFastFallback;
+        if (cpy > d.oc) fast_flush(d, cpy - d.oc, lane);
+        return int(cpy);
+      }
+      if (off > cpy) return kFastFallback;  // match < lowPrefix
+      fast_paint(d, cpy, cpy + ml, cpy - off, 0u, lane);
+      last_cpy = cpy;
+      last_lit_end = ls + ll;
+      op = cpy + ml;
+      last_mend = op;
+      ip = A;
+    }
+    if (ip >= csize) return kFastFallback;  // chain ran off the input without a last sequence
+    // advance to the segment holding ip (usually the next one)
+    const uint32_t nseg = ip & ~63u;
+    if (nseg == seg + 64u) {
+      cur = nxt;
+    } else {
+      cur = seg_parse(d, nseg, lane);
+    }
+    seg = nseg;
+    nxt = seg_parse(d, seg + 64u, lane);
+  }
+}

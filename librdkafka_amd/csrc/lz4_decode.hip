@@ -438,7 +438,7 @@ __global__ void lz4f_walk_kernel(const uint8_t *__restrict__ in, const uint64_t 
 // one block: raw copy or LZ4 decode, with the block checksum check first
 // (dstage_getCBlock verifies XXH32 before decoding, lz4frame.c:1596-1608)
 __device__ int run_block(const BlockInfo &b, uintptr_t frame, uintptr_t dst, uint32_t max_block,
-                         int realcap, int hist, lds_u8 *ring, int lane) {
+                         int realcap, int hist, lds_u8 *ring, lds_u8 *map, int lane) {
   const uintptr_t src = frame + b.src_off;
   if (b.flags & B_RAW) {
     if (int(b.csize) > realcap) return -2;
@@ -454,7 +454,8 @@ __device__ int run_block(const BlockInfo &b, uintptr_t frame, uintptr_t dst, uin
     if (uni(h) != b.xxh) return -1;
   }
   if (hist == 0 && !(b.flags & B_TRUNC) && realcap >= 0) {
-    const int r = decode_block_fast(src, b.csize, dst, max_block, uint32_t(realcap), ring, lane);
+    const int r =
+        decode_block_fast(src, b.csize, dst, max_block, uint32_t(realcap), ring, map, lane);
     if (r != kFastFallback) return r;
 #ifdef RDK_DEC_DEBUG
     if (lane == 0) printf("fallback src_off %u csize %u\n", b.src_off, b.csize);
@@ -477,9 +478,11 @@ __global__ __launch_bounds__(64 * kDecWaves) void lz4f_blocks_kernel(
     const FrameState *__restrict__ fs, BlockDesc *__restrict__ bd,
     const uint32_t *__restrict__ work_count, const uint32_t *__restrict__ work) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kDecWaves][kRing];
+  __shared__ __attribute__((aligned(16))) uint8_t maps[kDecWaves][64];
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
   lds_u8 *ring = (lds_u8 *)rings[uni(threadIdx.x >> 6)];
+  lds_u8 *map = (lds_u8 *)maps[uni(threadIdx.x >> 6)];
   const uint32_t gw = blockIdx.x * wpb + uni(threadIdx.x >> 6);
   const uint32_t items = uni(*work_count);
   (void)n;
@@ -493,7 +496,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void lz4f_blocks_kernel(
     b.src_off = uni(b.src_off); b.csize = uni(b.csize); b.flags = uni(b.flags); b.xxh = uni(b.xxh);
     const uint64_t slot = uint64_t(k) * mb;
     const int r = run_block(b, frame, obase + slot, mb, realcap_at(out_caps[f], slot, mb), 0, ring,
-                            lane);
+                            map, lane);
     if (lane == 0) bd[size_t(f) * kMaxDesc + k].result = r;
   }
 }
@@ -505,9 +508,11 @@ __global__ __launch_bounds__(64 * kDecWaves) void lz4f_seq_kernel(
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
     const uint32_t *__restrict__ out_caps, uint32_t n, FrameState *__restrict__ fs) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kDecWaves][kRing];
+  __shared__ __attribute__((aligned(16))) uint8_t maps[kDecWaves][64];
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
   lds_u8 *ring = (lds_u8 *)rings[uni(threadIdx.x >> 6)];
+  lds_u8 *map = (lds_u8 *)maps[uni(threadIdx.x >> 6)];
   const uint32_t gw = blockIdx.x * wpb + uni(threadIdx.x >> 6);
   for (uint32_t f = gw; f < n; f += gridDim.x * wpb) {
     const uint32_t status = uni(uint32_t(fs[f].fi.status));
@@ -527,7 +532,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void lz4f_seq_kernel(
       b.src_off = uni(b.src_off); b.csize = uni(b.csize); b.flags = uni(b.flags); b.xxh = uni(b.xxh);
       const int hist = linked ? int(produced < 65536u ? produced : 65536u) : 0;
       const int r = run_block(b, frame, obase + produced, mb, realcap_at(cap, produced, mb), hist,
-                              ring, lane);
+                              ring, map, lane);
       if (r < 0) { res = r; break; }
       produced += uint64_t(r);
     }

@@ -75,10 +75,12 @@ __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t nvalid, int lane
   // with in-order vmcnt retirement it has completed, so no wait is needed
   const uint32_t lb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live && lit) ? q : kNoAccess, 0, 0);
   const uint32_t fb = __builtin_amdgcn_raw_buffer_load_b8(d.rout, far ? q : kNoAccess, 0, 0);
+  asm volatile("" ::: "memory");  // ring bytes stored by other lanes
   const uint32_t rb = d.ring[q & kRingMask] & (ring_ok ? 0xFFu : 0u);
   // each lane's byte arrives in exactly one of the three (parked loads read 0)
   const uint32_t v = lb | fb | rb;
   if (live) d.ring[(d.oc + uint32_t(lane)) & kRingMask] = uint8_t(v);
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), d.rout, live ? d.oc + uint32_t(lane) : kNoAccess,
                                       0, 0);
 }
@@ -244,9 +246,40 @@ __device__ __forceinline__ SegCand seq_slow(rsrc_t rin, uint32_t csize, uint32_t
   return c;
 }
 
-// Decode one independent block.  Returns the decoded size or kFastFallback.
+// inclusive max over lanes 0..lane (DPP row shifts + row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  int x = int(v);
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true));   // row_shr:1
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true));   // row_shr:2
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true));   // row_shr:4
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true));   // row_shr:8
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return uint32_t(x);
+}
+
+// exclusive prefix sum over lanes (DPP), `total` = wave sum
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t &total) {
+  int x = int(v);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  total = uint32_t(__builtin_amdgcn_readlane(x, 63));
+  return uint32_t(x) - v;
+}
+
+// Decode one independent block, a whole 64-byte input segment at a time.
+// The chain walk only marks which candidate lanes are real sequences (one
+// v_readlane + one s_bitset per sequence); everything else is vector work
+// over the segment's sequences: output offsets by a lane prefix sum, the
+// reference's acceptance checks by ballot, and the output chunks painted
+// lane-per-byte (LDS scatter of sequence starts + max scan).
+// Returns the decoded size or kFastFallback.
 __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, uint32_t oend,
-                                 uint32_t realcap, lds_u8 *ring, int lane) {
+                                 uint32_t realcap, lds_u8 *ring, lds_u8 *map, int lane) {
   if (csize < 16u || csize > 65536u || oend > 65536u || oend < 64u) return kFastFallback;
   FastDec d;
   d.dst = dst;
@@ -258,52 +291,114 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
   d.realcap = realcap;
   d.oc = 0;
   d.dsrc = 0;
-
-  uint32_t op = 0, ip = 0;
+  uint32_t op = 0, ipn = 0;
   // the last non-final sequence decides the end-of-block margins
   uint32_t last_cpy = 0, last_lit_end = 0, last_mend = 0;
+  bool have_last = false;
   uint32_t seg = 0;
   SegCand cur = seg_parse(d, 0u, lane);
   SegCand nxt = seg_parse(d, 64u, lane);
   for (;;) {
-    // walk the chain through segment [seg, seg+64)
-    while (ip < seg + 64u) {
-      const uint32_t x = ip - seg;
-      uint32_t A = __builtin_amdgcn_readlane(cur.A, x);
-      uint32_t B, C;
-      if (A == kSeqComplex) {
-        const SegCand s = seq_slow(d.rin, d.csize, ip);
-        A = s.A; B = s.B; C = s.C;
-      } else {
-        B = __builtin_amdgcn_readlane(cur.B, x);
-        C = __builtin_amdgcn_readlane(cur.C, x);
+    // ---- walk: which candidate lanes are the real sequences of this segment
+    uint64_t M = 0;
+    uint32_t x = ipn - seg;
+    bool done = false;
+    while (x < 64u) {
+      uint32_t a = __builtin_amdgcn_readlane(cur.A, x);
+      if (a == kSeqComplex) {  // header too long for the lane window: parse it scalar
+        const SegCand s = seq_slow(d.rin, csize, seg + x);
+        const bool me = uint32_t(lane) == x;
+        cur.A = me ? s.A : cur.A;
+        cur.B = me ? s.B : cur.B;
+        cur.C = me ? s.C : cur.C;
+        a = s.A;
       }
-      if (A == kSeqBad) return kFastFallback;
-      const uint32_t ll = B & 0xFFFFu, ml = B >> 16, off = C & 0xFFFFu;
-      const uint32_t ls = ip + (C >> 16);
-      const uint32_t cpy = op + ll;
-      if (cpy + ml > realcap) return kFastFallback;  // the exact path reports the size error
-      fast_paint(d, op, cpy, ls, kLitTag, lane);
-      if (ml == 0u) {  // last sequence: literals end exactly at the input end
-        if (ls + ll != csize || cpy > oend) return kFastFallback;
-        if (op && (last_cpy > oend - uint32_t(kLz4MFLimit) ||
-                   last_lit_end > csize - uint32_t(2 + 1 + kLz4LastLiterals) ||
-                   last_mend > oend - uint32_t(kLz4LastLiterals)))
-          return kFastFallback;
-        if (cpy > d.oc) fast_flush(d, cpy - d.oc, lane);
-        return int(cpy);
+      if (a == kSeqBad) return kFastFallback;
+      M |= 1ull << x;
+      if (a == csize) {  // nothing can follow: must be the literals-only last sequence
+        done = true;
+        break;
       }
-      if (off > cpy) return kFastFallback;  // match < lowPrefix
-      fast_paint(d, cpy, cpy + ml, cpy - off, 0u, lane);
-      last_cpy = cpy;
-      last_lit_end = ls + ll;
-      op = cpy + ml;
-      last_mend = op;
-      ip = A;
+      x = a - seg;
     }
-    if (ip >= csize) return kFastFallback;  // chain ran off the input without a last sequence
-    // advance to the segment holding ip (usually the next one)
-    const uint32_t nseg = ip & ~63u;
+    const uint32_t xl = x;  // last member (only meaningful when done)
+#ifdef RDK_DEC_DEBUG
+    if (lane == 0 && seg < 512)
+      printf("seg %u ipn %u x %u M %016lx done %d op %u oc %u\n", seg, ipn, x, (unsigned long)M,
+             int(done), op, d.oc);
+#endif
+    // ---- the segment's sequences, one per member lane, in lane order
+    const bool mem = (M >> lane) & 1ull;
+    const uint32_t ll = cur.B & 0xFFFFu, ml = cur.B >> 16, off = cur.C & 0xFFFFu;
+    const uint32_t ls = seg + uint32_t(lane) + (cur.C >> 16);
+    uint32_t T;
+    const uint32_t ostart = op + wave_excl_sum(mem ? ll + ml : 0u, T);
+    const uint32_t cpy = ostart + ll;
+    if (ballot(mem && ml != 0u && off > cpy)) return kFastFallback;  // match < lowPrefix
+    if (op + T > realcap) return kFastFallback;  // the exact path reports the size error
+    const uint64_t nl = ballot(mem && ml != 0u);
+    if (nl) {
+      const int j = 63 - __builtin_clzll(nl);
+      last_cpy = __builtin_amdgcn_readlane(cpy, j);
+      last_lit_end = __builtin_amdgcn_readlane(ls + ll, j);
+      last_mend = __builtin_amdgcn_readlane(cpy + ml, j);
+      have_last = true;
+    }
+    if (done) {
+      const uint32_t lml = __builtin_amdgcn_readlane(ml, xl);
+      const uint32_t lcpy = __builtin_amdgcn_readlane(cpy, xl);
+      if (lml != 0u || lcpy > oend) return kFastFallback;
+      if (have_last && (last_cpy > oend - uint32_t(kLz4MFLimit) ||
+                        last_lit_end > csize - uint32_t(2 + 1 + kLz4LastLiterals) ||
+                        last_mend > oend - uint32_t(kLz4LastLiterals)))
+        return kFastFallback;
+    }
+    // ---- paint output [op, op+T) into 64-byte chunks, flushing full ones
+    const uint32_t op_new = op + T;
+    const uint32_t ffield = ll | (off << 16);
+    for (uint32_t c = d.oc; c < op_new; c += 64u) {
+      const uint32_t lo = op > c ? op : c;
+      const uint32_t hi = op_new < c + 64u ? op_new : c + 64u;
+      // member whose output starts at or before each lane's byte: starts in
+      // this chunk are scattered into the map and max-scanned; lanes before
+      // the chunk's first start take the member running into the chunk
+      // (compiler barriers: other lanes' LDS stores are invisible to the
+      // optimizer, which would otherwise forward map[lane] = 0 to the read)
+      map[lane] = 0;
+      asm volatile("" ::: "memory");
+      if (mem && ostart >= c && ostart < c + 64u && ll + ml != 0u) map[ostart - c] = uint8_t(lane + 1);
+      asm volatile("" ::: "memory");
+      uint32_t v = wave_incl_max(map[lane]);
+      const uint64_t before = ballot(mem && ostart < c && ll + ml != 0u);
+      const uint32_t carry = before ? uint32_t(64 - __builtin_clzll(before)) : 0u;
+      v = v ? v : carry;
+      const int idx = int(v ? v - 1u : 0u);
+      const uint32_t fo = uint32_t(__shfl(int(ostart), idx));
+      const uint32_t ff = uint32_t(__shfl(int(ffield), idx));
+      const uint32_t fl = uint32_t(__shfl(int(ls), idx));
+      const uint32_t o = c + uint32_t(lane);
+      const uint32_t rel = o - fo;
+      const uint32_t s = rel < (ff & 0xFFFFu) ? ((fl + rel) | kLitTag) : (o - (ff >> 16));
+      if (o >= lo && o < hi) d.dsrc = s;
+#ifdef RDK_DEC_DEBUG
+      if (seg == 64 && c == 64 && lane >= 10 && lane < 24)
+        printf("L%d mem %d ostart %u ll %u ml %u off %u ls %u | v %u fo %u ff %08x fl %u s %08x\n",
+               lane, int(mem), ostart, ll, ml, off, ls, v, fo, ff, fl, s);
+#endif
+      if (hi == c + 64u) {
+        fast_flush(d, 64u, lane);
+        d.oc = c + 64u;
+      }
+    }
+    op = op_new;
+    if (done) {
+      if (op > d.oc) fast_flush(d, op - d.oc, lane);
+      return int(op);
+    }
+    ipn = seg + x;
+    // ---- next segment (usually the prefetched one)
+    const uint32_t nseg = ipn & ~63u;
+    if (nseg >= csize) return kFastFallback;  // ran off the input without a last sequence
     if (nseg == seg + 64u) {
       cur = nxt;
     } else {

@@ -53,10 +53,29 @@ struct FastDec {
   uint32_t csize, oend, realcap;
   uint32_t oc;       // output position of the chunk being painted
   uint32_t dsrc;     // lane l: source of output byte oc+l (kLitTag | input pos, or output pos)
+  // the previous chunk, fetched but not yet written: its HBM loads stay in
+  // flight while the next chunk is painted
+  uint32_t pn, poc;  // live bytes (0: none) and output position
+  uint32_t plb, pfb, prb;
 };
 
-// Resolve, fetch and store output bytes [oc, oc+nvalid) of the painted chunk.
+// Write the pending chunk into the history ring and to HBM.  Each lane's byte
+// arrived in exactly one of its three sources (parked loads read 0).
+__device__ __forceinline__ void fast_retire(FastDec &d, int lane) {
+  if (!d.pn) return;
+  const bool live = uint32_t(lane) < d.pn;
+  const uint32_t v = d.plb | d.pfb | d.prb;
+  if (live) d.ring[(d.poc + uint32_t(lane)) & kRingMask] = uint8_t(v);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), d.rout, live ? d.poc + uint32_t(lane) : kNoAccess,
+                                      0, 0);
+  d.pn = 0;
+}
+
+// Resolve and fetch output bytes [oc, oc+nvalid) of the painted chunk; they
+// are written by the next retire, so the loads overlap the next painting.
 __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t nvalid, int lane) {
+  fast_retire(d, lane);  // the ring must hold everything before oc
   uint32_t src = d.dsrc;
   const bool live = uint32_t(lane) < nvalid;
   // match sources inside this chunk: pointer jumping, each step halves the
@@ -73,16 +92,12 @@ __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t nvalid, int lane
   const bool far = live && !lit && !ring_ok;
   // far history was stored >= kRing/64 chunks (>= 64 vector-memory ops) ago:
   // with in-order vmcnt retirement it has completed, so no wait is needed
-  const uint32_t lb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live && lit) ? q : kNoAccess, 0, 0);
-  const uint32_t fb = __builtin_amdgcn_raw_buffer_load_b8(d.rout, far ? q : kNoAccess, 0, 0);
+  d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live && lit) ? q : kNoAccess, 0, 0);
+  d.pfb = __builtin_amdgcn_raw_buffer_load_b8(d.rout, far ? q : kNoAccess, 0, 0);
   asm volatile("" ::: "memory");  // ring bytes stored by other lanes
-  const uint32_t rb = d.ring[q & kRingMask] & (ring_ok ? 0xFFu : 0u);
-  // each lane's byte arrives in exactly one of the three (parked loads read 0)
-  const uint32_t v = lb | fb | rb;
-  if (live) d.ring[(d.oc + uint32_t(lane)) & kRingMask] = uint8_t(v);
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), d.rout, live ? d.oc + uint32_t(lane) : kNoAccess,
-                                      0, 0);
+  d.prb = d.ring[q & kRingMask] & (ring_ok ? 0xFFu : 0u);
+  d.pn = nvalid;
+  d.poc = d.oc;
 }
 
 // output [a, b) takes its bytes from source positions s, s+1, ... (tag marks
@@ -291,6 +306,7 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
   d.realcap = realcap;
   d.oc = 0;
   d.dsrc = 0;
+  d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
   uint32_t op = 0, ipn = 0;
   // the last non-final sequence decides the end-of-block margins
   uint32_t last_cpy = 0, last_lit_end = 0, last_mend = 0;
@@ -393,6 +409,7 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
     op = op_new;
     if (done) {
       if (op > d.oc) fast_flush(d, op - d.oc, lane);
+      fast_retire(d, lane);
       return int(op);
     }
     ipn = seg + x;

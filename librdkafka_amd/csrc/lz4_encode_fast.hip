@@ -149,6 +149,7 @@ constexpr uint32_t kShortLit = 16;  // literal runs copied by their own lane
 struct BlockCtx {
   uintptr_t src, dst;
   rsrc_t r;            // the block's dwords
+  rsrc_t w;            // the block's output slot (byte stores; parked lanes write nothing)
   uint32_t sa;         // src & 3: byte offset of position 0 inside the resource
   int n, mfl, mlim, olimit;
   int p;               // parse position == anchor (end of the last match)
@@ -203,7 +204,6 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
                      __builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi) ==
                          __builtin_amdgcn_alignbyte(y.t[2], y.t[1], shc);
   const uint64_t vm = ballot(valid);
-  if (!vm) return true;
   int len = kFastLen;
 #pragma unroll
   for (int k = 6; k >= 1; --k) {
@@ -233,10 +233,11 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
     chosen |= 1ull << q;
     xr = q + L;
   }
-  if (!chosen) return true;
-  b.p = R + xr;
+  b.p = chosen ? R + xr : b.p;
 
-  // sequence fields of the chosen lanes
+  // sequence fields of the chosen lanes.  Every round runs the same store
+  // instructions (parked lanes write nothing), so the vmcnt bookkeeping never
+  // depends on how many sequences a round produced.
   const bool ch = (chosen >> lane) & 1ull;
   const uint64_t below = chosen & ((1ull << lane) - 1ull);
   const int pl = below ? 63 - __builtin_clzll(below) : lane;
@@ -248,45 +249,52 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
   bk = min(bk, min(lane - prev, y.c));            // literals only, inside the block
   const uint32_t lit = ch ? uint32_t(lane - bk - prev) : 0u;
   const uint32_t ml = uint32_t(len + bk);
-  const uint32_t sz = ch ? 3u + lit + ext_bytes(lit) + ext_bytes(ml - 4u) : 0u;
+  const uint32_t mc = ml - 4u;
+  const uint32_t lext = ext_bytes(lit);
+  const uint32_t sz = ch ? 3u + lit + lext + ext_bytes(mc) : 0u;
   uint32_t tot;
   const uint32_t o = wave_excl_scan(sz, tot);
   // keep room for the shortest possible last-literals token (lz4.c:1146)
   if (b.op + int(tot) + 1 > b.olimit) return false;
   const uint32_t lstart = uint32_t(R + prev);    // absolute literal start
-  // literal bytes: up to 4 (with the catch-up) sit in the lane's own back
-  // dword; longer short runs come from a 20-byte window
-  const bool in_reg = lit + uint32_t(bk) <= 4u;
+  const uint32_t tp = uint32_t(b.op) + o;        // token position in the block output
+  const uint32_t lp = tp + 1u + lext;            // first literal
+  const uint32_t fp = lp + lit;                  // offset field
+  __builtin_amdgcn_raw_buffer_store_b8(
+      uint8_t(((lit < 15u ? lit : 15u) << 4) | (mc < 15u ? mc : 15u)), b.w, ch ? tp : kNoLoad, 0, 0);
+  // up to 4 literals (with the catch-up) sit in the lane's own back dword
+  const bool in_reg = ch && lit + uint32_t(bk) <= 4u;
+  const uint32_t back = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi);
+  const uint32_t first = 4u - uint32_t(bk) - lit;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k)
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(back >> (8u * ((first + k) & 3u))), b.w,
+                                         (in_reg && k < lit) ? lp + k : kNoLoad, 0, 0);
+  // offset (LE16) and a single match-length byte (15 <= mc < 270)
+  const uint32_t off = uint32_t(i - y.c);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), b.w, ch ? fp : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), b.w, ch ? fp + 1u : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(mc - 15u), b.w,
+                                       (ch && mc >= 15u && mc < 270u) ? fp + 2u : kNoLoad, 0, 0);
+  // rare shapes, each behind a wave-uniform test
+  if (ballot(ch && lit >= 15u)) {  // literal length bytes: 255-runs + remainder
+    if (ch && lit >= 15u) put_len(b.dst + tp + 1u, lit);
+  }
+  if (ballot(ch && mc >= 270u)) {
+    if (ch && mc >= 270u) put_len(b.dst + fp + 2u, mc);
+  }
   const bool need_win = ch && !in_reg && lit <= kShortLit;
-  uint32_t w[5];
-  if (ballot(need_win)) load5(b.r, need_win ? ((lstart + b.sa) & ~3u) : kNoLoad, w);
-  if (ch) {
-    uintptr_t p = b.dst + uint32_t(b.op) + o;
-    const uint32_t mc = ml - 4u;
-    stb(p++, ((lit < 15u ? lit : 15u) << 4) | (mc < 15u ? mc : 15u));
-    if (lit >= 15u) p = put_len(p, lit);
-    if (in_reg) {
-      // bytes i-4..i-1 of the lane's window; the literals end bk before i
-      const uint32_t back = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi);
-      const uint32_t first = 4u - uint32_t(bk) - lit;
+  if (ballot(need_win)) {  // 5..16 literals: one 20-byte window per lane
+    uint32_t w[5];
+    load5(b.r, need_win ? ((lstart + b.sa) & ~3u) : kNoLoad, w);
+    const uint32_t sh = (lstart + b.sa) & 3u;
+    uint32_t v[4];
 #pragma unroll
-      for (uint32_t k = 0; k < 4; ++k)
-        if (k < lit) stb(p + k, back >> (8u * (first + k)));
-    } else if (lit <= kShortLit) {
-      const uint32_t sh = (lstart + b.sa) & 3u;
-      uint32_t v[4];
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-#pragma unroll
-      for (uint32_t k = 0; k < kShortLit; ++k)
-        if (k < lit) stb(p + k, v[k >> 2] >> (8u * (k & 3u)));
-    }
-    p += lit;
-    const uint32_t off = uint32_t(i - y.c);
-    stb(p, off & 0xFFu);
-    stb(p + 1, off >> 8);
-    p += 2;
-    if (mc >= 15u) put_len(p, mc);
+    for (uint32_t k = 0; k < kShortLit; ++k)
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), b.w,
+                                           (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
   }
   // long literal runs: the whole wave copies them one at a time
   uint64_t longm = ballot(ch && lit > kShortLit);
@@ -294,9 +302,9 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
     const int j = __builtin_ctzll(longm);
     longm &= longm - 1;
     const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
-    const uint32_t jo = __builtin_amdgcn_readlane(o, j);
+    const uint32_t jp = __builtin_amdgcn_readlane(lp, j);
     const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
-    wave_copy_bytes(b.dst + uint32_t(b.op) + jo + 1u + ext_bytes(jl), b.src + js, jl, lane);
+    wave_copy_bytes(b.dst + jp, b.src + js, jl, lane);
   }
   b.op += int(tot);
   return true;
@@ -323,6 +331,7 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
   b.dst = dst;
   const uintptr_t lo = src & ~uintptr_t(3);
   b.r = block_rsrc(lo, (src + uint32_t(n) + 3u) & ~uintptr_t(3));
+  b.w = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(dst), 0, n, 0x00020000);
   b.sa = uint32_t(src & 3u);
   b.n = n;
   b.mfl = n - kLz4MFLimit;        // last position a match may start (lz4.c:907)

@@ -151,6 +151,41 @@ int rdk_hip_lz4f_decompress(const void *d_in, const uint64_t *d_in_offs,
                             uint32_t *d_out_lens, int32_t *d_status, uint32_t n,
                             void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Producer batching front-end (north_star).  One
+ * producer per broker thread: a ring of `nslots` pinned host staging slots,
+ * each with its own device buffers and HIP stream.  produce() gathers one
+ * MsgVersion 2 batch -- the 61-byte header as the writer leaves it
+ * (rdkafka_msgset_writer.c:352-403 / finalize_MessageSet_v2_header :1251-1295:
+ * every field final except Length, the codec bits of Attributes and the CRC)
+ * plus its uncompressed records -- into the filling slot.  A full slot (or
+ * flush()) is launched as H2D -> LZ4F compress of every batch's records ->
+ * header finalize (the frame is dropped when larger than the records,
+ * rdkafka_msgset_writer.c:1179; Attributes |= LZ4 :1187; Length = size-12
+ * :1265) -> CRC32C finalize (:1229-1246) -> D2H, on the slot's stream, so
+ * the copies of one slot overlap the kernels of another.  poll() returns the
+ * finished batches in submission order; `data` points into the producer's
+ * pinned memory and stays valid until the next produce()/flush() call.
+ * ------------------------------------------------------------------------- */
+typedef struct rdk_hip_producer_s rdk_hip_producer_t;
+typedef struct rdk_hip_batch_s {
+  const void *data; /* finished v2 record batch (header + LZ4F or plain records) */
+  uint32_t len;     /* bytes = 12 + Length */
+  uint32_t crc;     /* the CRC32C stored big-endian at offset 17 */
+  uint64_t cookie;  /* as passed to produce() */
+} rdk_hip_batch_t;
+#define RDK_HIP_PRODUCER_EXACT 0 /* frames byte-identical to rd_kafka_lz4_compress */
+#define RDK_HIP_PRODUCER_FAST 1  /* rdk_hip_lz4f_compress_fast frames */
+#define RDK_HIP_E_BUSY (-5)      /* every slot is in flight: poll() first */
+rdk_hip_producer_t *rdk_hip_producer_new(int device, size_t slot_bytes, int nslots, int mode);
+int rdk_hip_producer_produce(rdk_hip_producer_t *p, const void *hdr61, const void *records,
+                             uint32_t len, uint64_t cookie);
+int rdk_hip_producer_flush(rdk_hip_producer_t *p);
+/* Up to `max` finished batches; block != 0 waits for the oldest slot.
+ * Returns the number of batches, or an RDK_HIP_E_* code. */
+int rdk_hip_producer_poll(rdk_hip_producer_t *p, rdk_hip_batch_t *out, int max, int block);
+void rdk_hip_producer_destroy(rdk_hip_producer_t *p);
+
 /* Deterministic synthetic workloads generated on the device (bench/tests).
  * v2 batches: n batches of `batch_size` bytes at i*batch_size: a valid 61-byte
  * v2 header (Magic 2, Length = batch_size-12, RecordCount) followed by

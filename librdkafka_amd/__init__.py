@@ -45,7 +45,8 @@ EXPORTED_SYMBOLS = (
     "rd_kafka_lz4_decompress", "rdk_hip_init", "rdk_hip_last_error", "rdk_hip_version",
     "rdk_hip_crc32c_ranges", "rdk_hip_msgset_v2_crc", "rdk_hip_lz4f_compress_bound",
     "rdk_hip_lz4f_compress", "rdk_hip_lz4f_compress_fast", "rdk_hip_lz4f_decompress",
-    "rdk_hip_gen_v2_batches",
+    "rdk_hip_gen_v2_batches", "rdk_hip_producer_new", "rdk_hip_producer_produce",
+    "rdk_hip_producer_flush", "rdk_hip_producer_poll", "rdk_hip_producer_destroy",
     "rdk_hip_gen_json",
 )
 
@@ -98,6 +99,16 @@ def lib():
         L.rdk_hip_lz4f_compress_fast.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp]
         L.rdk_hip_lz4f_decompress.restype = i32
         L.rdk_hip_lz4f_decompress.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
+    L.rdk_hip_producer_new.restype = vp
+    L.rdk_hip_producer_new.argtypes = [i32, sz, i32, i32]
+    L.rdk_hip_producer_produce.restype = i32
+    L.rdk_hip_producer_produce.argtypes = [vp, vp, vp, u32, C.c_uint64]
+    L.rdk_hip_producer_flush.restype = i32
+    L.rdk_hip_producer_flush.argtypes = [vp]
+    L.rdk_hip_producer_poll.restype = i32
+    L.rdk_hip_producer_poll.argtypes = [vp, vp, i32, i32]
+    L.rdk_hip_producer_destroy.restype = None
+    L.rdk_hip_producer_destroy.argtypes = [vp]
     L.rdk_hip_gen_v2_batches.restype = i32
     L.rdk_hip_gen_v2_batches.argtypes = [vp, u32, u32, C.c_uint64, vp]
     L.rdk_hip_gen_json.restype = None
@@ -289,6 +300,61 @@ def lz4f_decompress_batch(src, in_offs, in_lens, dst, out_offs, out_caps, out_le
                                          _ptr(out_offs), _ptr(out_caps), _ptr(out_lens),
                                          _ptr(status), int(in_offs.numel()), _stream(stream)),
            "lz4f_decompress")
+
+
+PRODUCER_EXACT, PRODUCER_FAST = 0, 1
+E_BUSY = -5
+
+
+class _Batch(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("len", C.c_uint32), ("crc", C.c_uint32),
+                ("cookie", C.c_uint64)]
+
+
+class Producer:
+    """Producer batching front-end (include/librdkafka_hip.h rdk_hip_producer_*):
+    a pinned staging ring whose slots run H2D -> LZ4F compress -> v2 header
+    finalize -> CRC32C -> D2H on their own streams.  One per broker thread."""
+
+    def __init__(self, device: int = 0, slot_bytes: int = 64 << 20, nslots: int = 4,
+                 mode: int = PRODUCER_FAST):
+        self._p = lib().rdk_hip_producer_new(device, slot_bytes, nslots, mode)
+        if not self._p:
+            raise EngineError("rdk_hip_producer_new: " + lib().rdk_hip_last_error().decode())
+        self._out = (_Batch * 4096)()
+
+    def produce(self, header61, records, cookie: int = 0) -> int:
+        """0, or E_BUSY when every slot is in flight (poll() first)."""
+        rc = lib().rdk_hip_producer_produce(self._p, header61, records, len(records), cookie)
+        if rc not in (0, E_BUSY):
+            _check(rc, "rdk_hip_producer_produce")
+        return rc
+
+    def flush(self) -> None:
+        _check(lib().rdk_hip_producer_flush(self._p), "rdk_hip_producer_flush")
+
+    def poll(self, block: bool = True, copy: bool = True):
+        """[(cookie, batch_bytes, crc)] of the finished batches (copies), or
+        [(cookie, (ptr, len), crc)] with copy=False (valid until the next
+        produce()/flush())."""
+        n = lib().rdk_hip_producer_poll(self._p, self._out, len(self._out), int(block))
+        if n < 0:
+            _check(n, "rdk_hip_producer_poll")
+        res = []
+        for b in self._out[:n]:
+            res.append((b.cookie, C.string_at(b.data, b.len) if copy else (b.data, b.len), b.crc))
+        return res
+
+    def close(self) -> None:
+        if self._p:
+            lib().rdk_hip_producer_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def gen_v2_batches(base, n: int, batch_size: int, seed: int = 0x5EED, stream=None) -> None:

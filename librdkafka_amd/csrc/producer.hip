@@ -1,0 +1,291 @@
+// producer.hip -- the producer-side batching front-end (north_star: "the
+// batching front-end collects ready batches from many toppars per broker
+// thread into a pinned host staging ring") and the device kernel that turns
+// compressed records into finished MsgVersion 2 record batches.
+//
+// Per broker thread one rdk_hip_producer_t owns a ring of `nslots` slots.
+// Each slot is pinned host staging in/out + device buffers + its own HIP
+// stream.  produce() gathers a batch (61-byte v2 header + records) into the
+// filling slot -- the rd_slice gather the reference does before
+// rd_kafka_lz4_compress (rdkafka_lz4.c:390) -- and a full slot is launched as
+//
+//   H2D -> LZ4F compress of every batch's records (exact or fast engine)
+//       -> v2_finalize_kernel: header copy, codec choice exactly as
+//          rd_kafka_msgset_writer_compress (rdkafka_msgset_writer.c:1179:
+//          a frame larger than the records is thrown away), Attributes |= LZ4
+//          (:1187), Length = size-12 (:1265-1267)
+//       -> CRC32C finalize over [21, 12+Length), stored BE at 17 (:1229-1246)
+//       -> D2H of the finished batches
+//
+// on the slot's stream, so slot k+1's copies overlap slot k's kernels.
+// poll() hands finished batches back in submission order.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "common.h"
+#include "lz4_device.h"
+
+namespace rdk {
+
+constexpr uint32_t kV2Hdr = 61;       // RD_KAFKAP_MSGSET_V2_SIZE (rdkafka_proto.h:540)
+constexpr uint32_t kV2OfLength = 8;   // RD_KAFKAP_MSGSET_V2_OF_Length
+constexpr uint32_t kV2OfAttr = 21;    // RD_KAFKAP_MSGSET_V2_OF_Attributes
+constexpr uint32_t kCodecLz4 = 3;     // RD_KAFKA_COMPRESSION_LZ4 (rdkafka_msg.h:48)
+
+// One workgroup per batch: out[out_off] = header, then either the frame the
+// compressor left at out_off+61 or (frame longer than the records) the
+// records themselves.
+__global__ __launch_bounds__(256) void v2_finalize_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ rec_offs,
+    const uint32_t *__restrict__ rec_lens, uint8_t *__restrict__ out,
+    const uint64_t *__restrict__ out_offs, const uint32_t *__restrict__ frame_lens,
+    uint32_t *__restrict__ batch_lens, uint32_t n) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint8_t *rec = in + rec_offs[i];
+    const uint8_t *hdr = rec - kV2Hdr;
+    uint8_t *o = out + out_offs[i];
+    const uint32_t len = rec_lens[i], flen = frame_lens[i];
+    const bool compressed = flen <= len;
+    const uint32_t payload = compressed ? flen : len;
+    if (!compressed)  // the frame slot holds >= len bytes, so the records fit
+      for (uint32_t k = t; k < len; k += blockDim.x) o[kV2Hdr + k] = rec[k];
+    if (t < kV2Hdr) {
+      uint32_t v = hdr[t];
+      const uint32_t length = kV2Hdr + payload - 12u;
+      if (t >= kV2OfLength && t < kV2OfLength + 4u) v = (length >> (8u * (3u - (t - kV2OfLength)))) & 0xFFu;
+      if (t == kV2OfAttr + 1u && compressed) v |= kCodecLz4;  // Attributes |= codec (low byte, BE)
+      if (t >= 17u && t < 21u) v = 0;  // CRC slot, filled by the CRC pass
+      o[t] = uint8_t(v);
+    }
+    if (t == 0) batch_lens[i] = kV2Hdr + payload;
+  }
+}
+
+namespace {
+
+enum SlotState { FREE = 0, FILLING, INFLIGHT };
+
+struct Slot {
+  hipStream_t s = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+  uint8_t *h_meta = nullptr, *d_meta = nullptr;
+  size_t in_used = 0, out_used = 0;
+  uint32_t nb = 0, polled = 0;
+  SlotState st = FREE;
+  std::vector<uint64_t> cookies;
+};
+
+}  // namespace
+
+size_t lz4f_compress_bound(size_t len);
+
+}  // namespace rdk
+
+using namespace rdk;
+
+struct rdk_hip_producer_s {
+  int device = 0, mode = 0;
+  size_t slot_bytes = 0, out_bytes = 0;
+  uint32_t max_batches = 0;
+  std::vector<Slot> slots;
+  int fill = 0;   // slot being filled
+  int next = 0;   // oldest slot not fully polled
+};
+
+namespace {
+
+// per-slot batch table (pinned host + device mirror), arrays of B entries:
+//   rec_offs, out_offs, frame_offs (u64) | caps, rec_lens, frame_lens,
+//   batch_lens, crcs (u32)
+struct Meta {
+  uint64_t *rec_offs, *out_offs, *frame_offs;
+  uint32_t *caps, *rec_lens, *frame_lens, *batch_lens, *crcs;
+};
+Meta meta_at(uint8_t *base, uint32_t B) {
+  Meta m;
+  m.rec_offs = reinterpret_cast<uint64_t *>(base);
+  m.out_offs = m.rec_offs + B;
+  m.frame_offs = m.out_offs + B;
+  m.caps = reinterpret_cast<uint32_t *>(m.frame_offs + B);
+  m.rec_lens = m.caps + B;
+  m.frame_lens = m.rec_lens + B;
+  m.batch_lens = m.frame_lens + B;
+  m.crcs = m.batch_lens + B;
+  return m;
+}
+size_t meta_bytes(uint32_t B) { return size_t(B) * (3 * 8 + 5 * 4); }
+
+size_t out_span(size_t len) { return (kV2Hdr + lz4f_compress_bound(len) + 255) & ~size_t(255); }
+
+int launch(rdk_hip_producer_s *p, Slot &sl) {
+  const uint32_t B = p->max_batches, n = sl.nb;
+  const Meta hm = meta_at(sl.h_meta, B), dm = meta_at(sl.d_meta, B);
+  RDK_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, sl.in_used, hipMemcpyHostToDevice, sl.s));
+  RDK_HIP_CHECK(hipMemcpyAsync(dm.rec_offs, hm.rec_offs, size_t(n) * 8, hipMemcpyHostToDevice, sl.s));
+  RDK_HIP_CHECK(hipMemcpyAsync(dm.out_offs, hm.out_offs, size_t(n) * 8, hipMemcpyHostToDevice, sl.s));
+  RDK_HIP_CHECK(hipMemcpyAsync(dm.frame_offs, hm.frame_offs, size_t(n) * 8, hipMemcpyHostToDevice, sl.s));
+  RDK_HIP_CHECK(hipMemcpyAsync(dm.caps, hm.caps, size_t(n) * 4, hipMemcpyHostToDevice, sl.s));
+  RDK_HIP_CHECK(hipMemcpyAsync(dm.rec_lens, hm.rec_lens, size_t(n) * 4, hipMemcpyHostToDevice, sl.s));
+  int rc;
+  if (p->mode == RDK_HIP_PRODUCER_FAST)
+    rc = rdk_hip_lz4f_compress_fast(sl.d_in, dm.rec_offs, dm.rec_lens, sl.d_out, dm.frame_offs,
+                                    dm.frame_lens, n, sl.s);
+  else
+    rc = rdk_hip_lz4f_compress(sl.d_in, dm.rec_offs, dm.rec_lens, sl.d_out, dm.frame_offs,
+                               dm.frame_lens, n, 0, sl.s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(v2_finalize_kernel, dim3(n < 4096u ? n : 4096u), dim3(256), 0, sl.s, sl.d_in,
+                     dm.rec_offs, dm.rec_lens, sl.d_out, dm.out_offs, dm.frame_lens,
+                     dm.batch_lens, n);
+  RDK_HIP_CHECK(hipGetLastError());
+  // CRC32C over [21, 12+Length) of each finished batch, stored BE at 17
+  if ((rc = rdk_hip_msgset_v2_crc(sl.d_out, dm.out_offs, dm.caps, dm.crcs, n,
+                                  RDK_HIP_V2_CRC_FINALIZE, sl.s)))
+    return rc;
+  RDK_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sl.out_used, hipMemcpyDeviceToHost, sl.s));
+  RDK_HIP_CHECK(hipMemcpyAsync(hm.batch_lens, dm.batch_lens, size_t(n) * 4, hipMemcpyDeviceToHost, sl.s));
+  RDK_HIP_CHECK(hipMemcpyAsync(hm.crcs, dm.crcs, size_t(n) * 4, hipMemcpyDeviceToHost, sl.s));
+  RDK_HIP_CHECK(hipEventRecord(sl.done, sl.s));
+  sl.st = INFLIGHT;
+  sl.polled = 0;
+  return 0;
+}
+
+void release(rdk_hip_producer_s *p) {
+  for (Slot &sl : p->slots) {
+    if (sl.s) (void)hipStreamSynchronize(sl.s);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+    if (sl.s) (void)hipStreamDestroy(sl.s);
+    if (sl.h_in) (void)hipHostFree(sl.h_in);
+    if (sl.h_out) (void)hipHostFree(sl.h_out);
+    if (sl.h_meta) (void)hipHostFree(sl.h_meta);
+    if (sl.d_in) (void)hipFree(sl.d_in);
+    if (sl.d_out) (void)hipFree(sl.d_out);
+    if (sl.d_meta) (void)hipFree(sl.d_meta);
+  }
+}
+
+}  // namespace
+
+RDK_API rdk_hip_producer_t *rdk_hip_producer_new(int device, size_t slot_bytes, int nslots,
+                                                  int mode) {
+  if (rdk_hip_init(device)) return nullptr;
+  if (nslots < 1 || slot_bytes < 4096 || (mode != RDK_HIP_PRODUCER_EXACT && mode != RDK_HIP_PRODUCER_FAST)) {
+    set_error(RDK_HIP_E_INVAL, "producer: bad arguments");
+    return nullptr;
+  }
+  rdk_hip_producer_s *p = new (std::nothrow) rdk_hip_producer_s();
+  if (!p) return nullptr;
+  p->device = device;
+  p->mode = mode;
+  p->slot_bytes = slot_bytes;
+  p->max_batches = uint32_t(slot_bytes / 512 + 64);
+  // worst case: every batch at most slot_bytes, spans rounded up
+  p->out_bytes = out_span(slot_bytes) + size_t(p->max_batches) * 512;
+  p->slots.resize(size_t(nslots));
+  const size_t mb = meta_bytes(p->max_batches);
+  for (Slot &sl : p->slots) {
+    if (hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&sl.h_in), slot_bytes, 0) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&sl.h_out), p->out_bytes, 0) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&sl.h_meta), mb, 0) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&sl.d_in), slot_bytes + 256) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&sl.d_out), p->out_bytes) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&sl.d_meta), mb) != hipSuccess) {
+      set_error(RDK_HIP_E_NOMEM, "producer: staging allocation failed");
+      release(p);
+      delete p;
+      return nullptr;
+    }
+  }
+  return p;
+}
+
+RDK_API int rdk_hip_producer_produce(rdk_hip_producer_t *p, const void *hdr61, const void *records,
+                                     uint32_t len, uint64_t cookie) {
+  if (!p || !hdr61 || (!records && len)) return set_error(RDK_HIP_E_INVAL, "null pointer");
+  const size_t need_in = (kV2Hdr + size_t(len) + 64 + 15) & ~size_t(15);
+  const size_t need_out = out_span(len);
+  if (need_in > p->slot_bytes || need_out > p->out_bytes)
+    return set_error(RDK_HIP_E_INVAL, "batch of %u bytes exceeds the slot", len);
+  Slot *sl = &p->slots[size_t(p->fill)];
+  if (sl->st == FILLING && (sl->in_used + need_in > p->slot_bytes ||
+                            sl->out_used + need_out > p->out_bytes || sl->nb == p->max_batches)) {
+    int rc = rdk_hip_producer_flush(p);
+    if (rc) return rc;
+    sl = &p->slots[size_t(p->fill)];
+  }
+  if (sl->st == INFLIGHT) return RDK_HIP_E_BUSY;  // the ring is full: poll() first
+  if (sl->st == FREE) {
+    sl->st = FILLING;
+    sl->in_used = sl->out_used = 0;
+    sl->nb = 0;
+    sl->cookies.clear();
+  }
+  Meta hm = meta_at(sl->h_meta, p->max_batches);
+  std::memcpy(sl->h_in + sl->in_used, hdr61, kV2Hdr);
+  if (len) std::memcpy(sl->h_in + sl->in_used + kV2Hdr, records, len);
+  hm.rec_offs[sl->nb] = sl->in_used + kV2Hdr;
+  hm.rec_lens[sl->nb] = len;
+  hm.out_offs[sl->nb] = sl->out_used;
+  hm.frame_offs[sl->nb] = sl->out_used + kV2Hdr;
+  hm.caps[sl->nb] = uint32_t(need_out);
+  sl->cookies.push_back(cookie);
+  sl->in_used += need_in;
+  sl->out_used += need_out;
+  sl->nb++;
+  return RDK_HIP_OK;
+}
+
+RDK_API int rdk_hip_producer_flush(rdk_hip_producer_t *p) {
+  if (!p) return set_error(RDK_HIP_E_INVAL, "null producer");
+  Slot &sl = p->slots[size_t(p->fill)];
+  if (sl.st != FILLING || !sl.nb) return RDK_HIP_OK;
+  int rc = launch(p, sl);
+  if (rc) return rc;
+  p->fill = (p->fill + 1) % int(p->slots.size());
+  return RDK_HIP_OK;
+}
+
+RDK_API int rdk_hip_producer_poll(rdk_hip_producer_t *p, rdk_hip_batch_t *out, int max,
+                                  int block) {
+  if (!p || (!out && max > 0)) return set_error(RDK_HIP_E_INVAL, "null pointer");
+  int got = 0;
+  while (got < max) {
+    Slot &sl = p->slots[size_t(p->next)];
+    if (sl.st != INFLIGHT) break;
+    if (sl.polled == 0) {
+      const hipError_t e = block ? hipEventSynchronize(sl.done) : hipEventQuery(sl.done);
+      if (e == hipErrorNotReady) break;
+      if (e != hipSuccess)
+        return set_error(RDK_HIP_E_HIP, "producer slot: %s", hipGetErrorString(e));
+    }
+    Meta hm = meta_at(sl.h_meta, p->max_batches);
+    while (got < max && sl.polled < sl.nb) {
+      const uint32_t i = sl.polled++;
+      out[got].data = sl.h_out + hm.out_offs[i];
+      out[got].len = hm.batch_lens[i];
+      out[got].crc = hm.crcs[i];
+      out[got].cookie = sl.cookies[i];
+      ++got;
+    }
+    if (sl.polled == sl.nb) {
+      sl.st = FREE;
+      p->next = (p->next + 1) % int(p->slots.size());
+    }
+  }
+  return got;
+}
+
+RDK_API void rdk_hip_producer_destroy(rdk_hip_producer_t *p) {
+  if (!p) return;
+  release(p);
+  delete p;
+}

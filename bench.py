@@ -225,6 +225,91 @@ def bench_consumer(args, rank, world, n=None):
             "alg_bytes": csum + (csum + 61 * n) + n * JSON_BATCH}
 
 
+def bench_producer(args, rank, world, n=None, threads=None, mode=1, slot_mib=None):
+    """configs[4] (full producer pipeline), bounded: n toppars per GPU each
+    hand one linger-accumulated 1 MiB batch of JSON records (61-byte v2
+    header + records in host memory) to the producer front-end.  `threads`
+    broker threads, each with its own rdk_hip_producer_t (pinned staging ring
+    of 4 slots, one HIP stream per slot), gather the batches into
+    the ring; slots run H2D -> LZ4F compress -> v2 finalize -> CRC32C -> D2H
+    while the next slot fills.  Timed: first produce() to the last finished
+    batch polled.  PCIe-inclusive by construction."""
+    import threading
+    import numpy as np
+    import librdkafka_amd as L
+    from librdkafka_amd import workload as W
+    n = n or args.partitions // world
+    # measured sweep (threads x slot MiB): 1x256 17, 2x128 20.3, 2x64 18.7, 4x64 16.2,
+    # 4x128 14.7, 8x16 11.6 GB/s -- host gather + PCIe bound, more streams than
+    # the 4 hardware queues serialise the compress launches
+    threads = threads or int(os.environ.get("RDK_BENCH_PRODUCER_THREADS", "2"))
+    slot_mib = slot_mib or int(os.environ.get("RDK_BENCH_PRODUCER_SLOT_MIB", "128"))
+    distinct = 8
+    recs = [L.gen_json(JSON_BATCH, 42 + rank * 97 + j) for j in range(distinct)]
+    hdrs = [W.v2_header(i, 61 + JSON_BATCH) for i in range(n)]
+    parts = [list(range(t, n, threads)) for t in range(threads)]
+    prods = [L.Producer(0, slot_bytes=slot_mib << 20, nslots=4, mode=mode) for _ in range(threads)]
+    out_bytes = [0] * threads
+
+    def run(t, todo, count_out):
+        p = prods[t]
+        done = 0
+        for i in todo:
+            while p.produce(hdrs[i], recs[i % distinct], i) == L.E_BUSY:
+                for _, (_, ln), _ in p.poll(block=True, copy=False):
+                    done += 1
+                    if count_out:
+                        out_bytes[t] += ln
+        p.flush()
+        while done < len(todo):
+            for _, (_, ln), _ in p.poll(block=True, copy=False):
+                done += 1
+                if count_out:
+                    out_bytes[t] += ln
+
+    def once(count_out=False):
+        ths = [threading.Thread(target=run, args=(t, parts[t], count_out)) for t in range(threads)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+
+    once()  # warm-up: staging allocations, first-touch of pinned memory
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        once(count_out=True)
+    wall = (time.perf_counter() - t0) / args.steps
+    barrier(world)
+    for p in prods:
+        p.close()
+    total = n * JSON_BATCH
+    return {"ms": wall * 1e3, "kernel_ms": None, "bytes": total, "records": n,
+            "out_bytes": sum(out_bytes) // args.steps, "threads": threads}
+
+
+def pcie_rates(nbytes=256 << 20, reps=4):
+    """Pinned host <-> device copy rates on this GPU (north_star: reported
+    separately, never folded into the device-resident value)."""
+    import torch
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    d.copy_(h, non_blocking=True)
+    h.copy_(d, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        h.copy_(d, non_blocking=True)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    return {"h2d_GBps": round(reps * nbytes / (t1 - t0) / 1e9, 1),
+            "d2h_GBps": round(reps * nbytes / (t2 - t1) / 1e9, 1), "bytes": nbytes}
+
+
 def cpu_baseline_crc(buf, n, size, seconds=8.0):
     """The oracle's restatement of crc32c_hw (crc32c.c:255-338, SSE4.2 3-way),
     on CPU_THREADS host threads over a bounded 1 GiB sample of the batches."""
@@ -294,11 +379,16 @@ def cpu_baseline_lz4(kind, n=64, seconds=4.0):
 
 
 def leg_line(name, res, steps, world, cpu=None):
-    ach = res["alg_bytes"] / (res["kernel_ms"] / 1e3) / 1e9
     d = {"GB_per_s": round(res["bytes"] * world / (res["ms"] / 1e3) / 1e9, 2),
-         "ms_per_step": round(res["ms"], 3), "batches": res["records"] * world,
-         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
+         "ms_per_step": round(res["ms"], 3), "batches": res["records"] * world}
+    if res.get("kernel_ms"):
+        ach = res["alg_bytes"] / (res["kernel_ms"] / 1e3) / 1e9
+        d["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
+    if "out_bytes" in res:
+        d["compression_ratio"] = round(res["bytes"] / max(1, res["out_bytes"]), 3)
+        d["pcie_inclusive"] = True
+        d["host_threads"] = res["threads"]
     if "ratio" in res:
         d["compression_ratio"] = round(res["ratio"], 3)
     if cpu:
@@ -332,7 +422,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="crc", choices=["crc", "lz4c", "lz4c_fast", "consumer"])
+    ap.add_argument("--workload", default="crc", choices=["crc", "lz4c", "lz4c_fast", "consumer", "producer"])
     ap.add_argument("--batches", type=int, default=CRC_BATCHES)
     ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -351,14 +441,18 @@ def main():
     L.init(local_rank)
 
     if args.workload != "crc":
-        res = bench_lz4c(args, rank, world, fast=args.workload == "lz4c_fast") \
-            if args.workload.startswith("lz4c") else bench_consumer(args, rank, world)
+        if args.workload.startswith("lz4c"):
+            res = bench_lz4c(args, rank, world, fast=args.workload == "lz4c_fast")
+        elif args.workload == "producer":
+            res = bench_producer(args, rank, world)
+        else:
+            res = bench_consumer(args, rank, world)
         t_max = max_over_ranks(res["ms"], world)
         if rank == 0:
             cpu = None
             if not args.no_cpu_baseline and world == 1:
-                cpu = cpu_baseline_lz4("compress" if args.workload.startswith("lz4c")
-                                      else "decompress")
+                cpu = cpu_baseline_lz4("decompress" if args.workload == "consumer"
+                                       else "compress")
             res["ms"] = t_max
             print(json.dumps({"workload": args.workload, "n_gpus": world, "steps": args.steps,
                               **leg_line(args.workload, res, args.steps, world, cpu)}), flush=True)
@@ -407,6 +501,7 @@ def main():
             buf, n, size = res["host_sample"]
             line["cpu_baseline"] = cpu_baseline_crc(buf, n, size)
         del res
+        line["pcie_pinned"] = pcie_rates()
         if not args.no_legs and world == 1:
             # the LZ4F legs of the same path (configs[2], configs[3]) at 256 x 1 MiB
             sub = argparse.Namespace(steps=3, warmup=1, partitions=256)
@@ -417,7 +512,11 @@ def main():
                 "lz4f_compress_fast_1MiB_json": leg_line(
                     "lz4c_fast", bench_lz4c(sub, rank, world, fast=True), 3, 1, cpu("compress")),
                 "consumer_crc_verify_lz4f_decompress_1MiB": leg_line(
-                    "consumer", bench_consumer(sub, rank, world), 3, 1, cpu("decompress")),
+                    "consumer", bench_consumer(argparse.Namespace(steps=3, warmup=1, partitions=1024),
+                                               rank, world), 3, 1, cpu("decompress")),
+                "producer_pipeline_1MiB_json_pcie": leg_line(
+                    "producer", bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512),
+                                               rank, world), 2, 1, cpu("compress")),
             }
         print(json.dumps(line), flush=True)
     if world > 1:

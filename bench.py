@@ -400,12 +400,13 @@ def leg_line(name, res, steps, world, cpu=None):
 # (scripts/profile_crc.sh -> scripts/pmc_summary.py; FETCH_SIZE x2 on gfx950).
 # Counters cannot be read in-process, so the committed summary of the same
 # kernel build and batch shape is used; null when they do not match.
-CRC_PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_crc_v3", "summary.json")
+CRC_VARIANT = "v1" if os.environ.get("RDK_HIP_CRC_V1") else "v" + os.environ.get("RDK_HIP_CRC_V", "4")
+CRC_KERNEL = ("crc32c_msgset_v2_v4_kernel<FINALIZE>" if CRC_VARIANT == "v4"
+              else "crc32c_msgset_v2_kernel<%d, FINALIZE>" % int(CRC_VARIANT[1:]))
+CRC_PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_crc_%s" % CRC_VARIANT, "summary.json")
 
 
 def pmc_traffic(path, alg_bytes):
-    if os.environ.get("RDK_HIP_CRC_V1"):
-        return None, None
     try:
         with open(path) as f:
             s = json.load(f)
@@ -489,7 +490,7 @@ def main():
             "msgs_per_s": round(args.batches * world / (t_max / 1e3), 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "crc32c_msgset_v2_kernel<FINALIZE>",
+                         "traffic": None, "kernel": CRC_KERNEL,
                          "alg_bytes_per_launch": res["alg_bytes"]},
             "cpu_baseline": None,
         }

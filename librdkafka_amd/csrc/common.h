@@ -45,6 +45,7 @@ int ensure_desc(Ctx *c, size_t bytes);
 const uint32_t *crc_tables_dev(int device);     // v1: byte slicing-by-16 image
 const uint32_t *crc_tables_v3_dev(int device);  // v3: rotated-nibble image
 // x^(2^k) mod P table (k = 0..63) for arbitrary-length shifts.
+const uint32_t *crc_tables_v4_dev(int device);  // v4: 16-lane-group byte-table image
 const uint32_t *crc_x2n_dev(int device);
 
 // Aborts the process with a message (drop-in symbols have no error channel).

@@ -27,6 +27,7 @@
 #include "crc32c_tables.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace rdk {
 
@@ -291,6 +292,185 @@ __device__ __attribute__((always_inline)) uint32_t wave_crc_v3(uintptr_t s, uint
   return final ? ~x : x;
 }
 
+// ---------------------------------------------------------------- v4 path
+// Four ranges per wavefront, one per 16-lane group (crc32c_tables.h "v4 image").
+// Per 16-byte vector a lane does 16 LDS lookups whose addresses are one v_perm_b32
+// each, and 8 xor3: half the LDS cycles of v3 per byte.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kNoLoad = 0x80000000u;  // buffer offset past num_records: reads 0
+constexpr uint32_t kV4Span = 0x7f000000u;  // ranges of one pass lie within this of its base
+constexpr int kV4Prefetch = 8;             // 256-byte group steps in flight per lane
+
+// selector: byte 0 <- C byte t (4c | 0x80t), byte 1 <- register byte q, byte 2 <- C byte 2
+// (0x01) for the upper half, else 0; byte 3 <- 0
+typedef __attribute__((address_space(3))) const uint8_t lds_c8;
+// LDS read at byte offset a + off of the kernel's table image Lb (a static array, the
+// kernel's only LDS object: reads through it keep the allocation alive and fold to
+// absolute addresses)
+__device__ __forceinline__ uint32_t lds4(const lds_u32 *Lb, uint32_t a, uint32_t off) {
+  return *reinterpret_cast<const lds_u32 *>(reinterpret_cast<lds_c8 *>(Lb) + a + off);
+}
+
+template <int Q> constexpr uint32_t v4_sel() {
+  return uint32_t(Q & 1) | (uint32_t(4 + Q) << 8) | (uint32_t((Q >> 1) ? 2 : 12) << 16) |
+         (12u << 24);
+}
+
+__device__ __forceinline__ uint32_t v4_step(const lds_u32 *Lb, uint32_t r, uint32_t w, uint32_t C) {
+  const uint32_t a = lds4(Lb, __builtin_amdgcn_perm(r, C, v4_sel<0>()), 0);
+  const uint32_t b = lds4(Lb, __builtin_amdgcn_perm(r, C, v4_sel<1>()), 0);
+  const uint32_t c = lds4(Lb, __builtin_amdgcn_perm(r, C, v4_sel<2>()), 0);
+  const uint32_t d = lds4(Lb, __builtin_amdgcn_perm(r, C, v4_sel<3>()), 0);
+  return xor3(xor3(a, b, c), d, w);
+}
+
+__device__ __forceinline__ uint32_t v4_z4(const lds_u32 *Lb, uint32_t x) {
+  return lds4(Lb, (x & 0xffu) << 2, kV4Z4) ^ lds4(Lb, ((x >> 8) & 0xffu) << 2, kV4Z4 + 1024) ^
+         lds4(Lb, ((x >> 16) & 0xffu) << 2, kV4Z4 + 2048) ^ lds4(Lb, (x >> 24) << 2, kV4Z4 + 3072);
+}
+
+__device__ __forceinline__ uint32_t v4_fin(const lds_u32 *Lb, uint32_t x, uint32_t lc4) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r ^= lds4(Lb, (((x >> (4 * i)) & 15u) << 7) | lc4, kV4Fin + 2048 * i);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t v4_t0(const lds_u32 *Lb, uint32_t r, uint32_t byte) {
+  return lds4(Lb, ((r ^ byte) & 0xffu) << 2, kV4T0) ^ (r >> 8);
+}
+
+// xor over the 16 lanes of a DPP row (= one group)
+__device__ __forceinline__ uint32_t row_xor(uint32_t v) {
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x122, 0xf, 0xf, false);  // row_ror:2
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x121, 0xf, 0xf, false);  // row_ror:1
+  return v;
+}
+
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(v), l);
+  const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(v >> 32), l);
+  return (uint64_t(hi) << 32) | lo;
+}
+
+// Raw CRC register (before the final inversion) of the group's range [s, e), whose
+// running crc is injected as ninit = ~init; valid in every lane of the group.  `active`
+// must be uniform within a group.  Groups whose ranges lie within kV4Span of each
+// other share one pass over their longest range (shorter ones start with zero
+// vectors, which leave a raw register unchanged); others take further passes.
+__device__ __attribute__((always_inline)) uint32_t group_crc_v4(uintptr_t s, uintptr_t e,
+                                                               uint32_t ninit, bool active,
+                                                               int lane, const lds_u32 *Lb) {
+  typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
+  const uint32_t l = uint32_t(lane) & 15u;
+  const uint32_t lc4 = (uint32_t(lane) & 31u) << 2;
+  const uint32_t C = lc4 | ((lc4 | 0x80u) << 8) | (1u << 16);
+  const size_t len = active ? e - s : 0;
+  const bool big = active && len >= size_t(kCrcSmall);
+  if (active && !big) {  // short range: byte-serial, every lane of the group alike
+    uint32_t c = ninit;
+    gbl_u8 *p = (gbl_u8 *)s;
+    for (size_t i = 0; i < len; ++i) c = v4_t0(Lb, c, p[i]);
+    return c;
+  }
+  const uintptr_t A = s & ~uintptr_t(15), B = e & ~uintptr_t(15);
+  const uint32_t K = big ? uint32_t(((B - A) >> 4) + 15u) >> 4 : 0u;  // 256-byte steps
+  uint32_t F0 = 0, F1 = 0, F2 = 0, F3 = 0;
+  // groups still to do: one bit per group leader lane
+  uint64_t todo = __builtin_amdgcn_ballot_w64(big && l == 0);
+  while (todo) {
+    // pass base: the lowest A among the remaining groups
+    uintptr_t sb = ~uintptr_t(0);
+    for (uint64_t t = todo; t; t &= t - 1) {
+      const uintptr_t a = rdlane64(A, int(__builtin_ctzll(t)));
+      sb = a < sb ? a : sb;
+    }
+    const bool inpass = big && ((todo >> (lane & 48)) & 1u) && B - sb < kV4Span;
+    const uint64_t pm = __builtin_amdgcn_ballot_w64(inpass && l == 0);
+    todo &= ~pm;
+    uint32_t Kmax = 0;
+    for (uint64_t t = pm; t; t &= t - 1) {
+      const uint32_t k = __builtin_amdgcn_readlane(K, int(__builtin_ctzll(t)));
+      Kmax = k > Kmax ? k : Kmax;
+    }
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(sb), 0,
+                                                        int(kNoLoad), 0x00020000);
+    // lane offsets relative to sb: vector k at o0 + 256k; below lowA (before the range,
+    // including the shorter ranges' leading steps) the load is parked and reads 0
+    // (lanes outside the pass: INT32_MIN, so that every offset stays >= kNoLoad)
+    const int32_t o0 =
+        inpass ? int32_t(uint32_t(B - sb) - kV4Stride * Kmax + 16u * l) : int32_t(kNoLoad);
+    const int32_t lowA = inpass ? int32_t(uint32_t(A - sb)) : 0x7fffffff;
+    const uint32_t srel = uint32_t(s - sb);
+    auto off = [&](uint32_t k) -> uint32_t {
+      const int32_t o = o0 + int32_t(kV4Stride * k);
+      return (k < Kmax && o >= lowA) ? uint32_t(o) : kNoLoad;
+    };
+    // last step holding a head vector ([A, A+32) of some range in the pass): blocks after it
+    // load unconditionally and skip the head check
+    uint32_t khead = 0;
+    {
+      const int32_t kl = inpass ? (lowA + 31 - o0) >> 8 : 0;  // per group leader (l = 0)
+      for (uint64_t t = pm; t; t &= t - 1) {
+        const int32_t k = __builtin_amdgcn_readlane(kl, int(__builtin_ctzll(t)));
+        khead = uint32_t(k) > khead ? uint32_t(k) : khead;
+      }
+    }
+    uint32_t R0 = 0, R1 = 0, R2 = 0, R3 = 0;
+    u32x4 buf[kV4Prefetch];
+#pragma unroll
+    for (int j = 0; j < kV4Prefetch; ++j)
+      buf[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off(uint32_t(j)), 0, 2);
+    // one block = kV4Prefetch steps; CHK: steps may hold heads, loads may fall outside
+    auto block = [&](uint32_t k0, auto chk) __attribute__((always_inline)) {
+      constexpr bool CHK = decltype(chk)::value;
+#pragma unroll
+      for (int j = 0; j < kV4Prefetch; ++j) {
+        const uint32_t k = k0 + uint32_t(j);
+        if (!CHK || k < Kmax) {
+          u32x4 w = buf[j];
+          const uint32_t kn = k + kV4Prefetch;
+          buf[j] = __builtin_amdgcn_raw_buffer_load_b128(
+              rs, CHK ? off(kn) : uint32_t(o0 + int32_t(kV4Stride * kn)), 0, 2);
+          if (CHK) {
+            const int32_t o = o0 + int32_t(kV4Stride * k);
+            if (o >= lowA && o < lowA + 32) {  // head: zero bytes before s, inject ninit
+              const uintptr_t d = uintptr_t(uint32_t(o));
+              w.x = head_fix(w.x, d, srel, ninit);
+              w.y = head_fix(w.y, d + 4, srel, ninit);
+              w.z = head_fix(w.z, d + 8, srel, ninit);
+              w.w = head_fix(w.w, d + 12, srel, ninit);
+            }
+          }
+          R0 = v4_step(Lb, R0, w.x, C);
+          R1 = v4_step(Lb, R1, w.y, C);
+          R2 = v4_step(Lb, R2, w.z, C);
+          R3 = v4_step(Lb, R3, w.w, C);
+        }
+      }
+    };
+    for (uint32_t k0 = 0; k0 < Kmax; k0 += kV4Prefetch) {
+      if (k0 > khead && k0 + 2 * kV4Prefetch <= Kmax) block(k0, std::false_type{});
+      else block(k0, std::true_type{});
+    }
+    F0 ^= R0;  // lanes outside the pass kept R = 0
+    F1 ^= R1;
+    F2 ^= R2;
+    F3 ^= R3;
+  }
+  // combine the four dword streams, place lane l, reduce the group
+  uint32_t r = v4_z4(Lb, v4_z4(Lb, v4_z4(Lb, F0) ^ F1) ^ F2) ^ F3;
+  r = row_xor(v4_fin(Lb, r, lc4));
+  // fold the <16-byte tail [B, e) byte by byte (crc32c.c:131)
+  if (big) {
+    gbl_u8 *p = (gbl_u8 *)B;
+    for (uint32_t i = 0, t = uint32_t(e - B); i < t; ++i) r = v4_t0(Lb, r, p[i]);
+  }
+  return r;
+}
+
 template <int V>
 __device__ __forceinline__ uint32_t wave_crc_v(uintptr_t s, uintptr_t e, uint32_t init,
                                                bool inject, bool final, const lds_u32 *L,
@@ -426,14 +606,105 @@ __global__ __launch_bounds__(crc_block<V>(), 8) void crc32c_msgset_v2_kernel(
   }
 }
 
+// ---- v4 kernels: 16 waves x 4 groups = 64 ranges per workgroup round; the
+// 148 KiB table image allows one workgroup per CU
+constexpr int kV4Block = 1024;
+constexpr int kV4Groups = kV4Block / 16;
+
+__device__ __forceinline__ void load_tables_v4(uint32_t *L, const uint32_t *g) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(g);
+  uint4 *dst = reinterpret_cast<uint4 *>(L);
+  for (int i = threadIdx.x; i < kCrcV4Words / 4; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kV4Block, 1) void crc32c_ranges_v4_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint32_t *__restrict__ lens, const uint32_t *__restrict__ init,
+    uint32_t *__restrict__ out, uint32_t n, const uint32_t *__restrict__ gtab) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[kCrcV4Words];  // the kernel's only LDS: at 0
+  load_tables_v4(L, gtab);
+  const int lane = threadIdx.x & 63;
+  const uint32_t grp = blockIdx.x * kV4Groups + (threadIdx.x >> 4);
+  const uint32_t stride = gridDim.x * kV4Groups;
+  // every wave runs the same number of rounds (uniform trip count)
+  for (uint32_t i0 = blockIdx.x * kV4Groups; i0 < n; i0 += stride) {
+    const uint32_t i = i0 - blockIdx.x * kV4Groups + grp;
+    const bool active = i < n;
+    uintptr_t s = 0, e = 0;
+    uint32_t c0 = 0;
+    if (active) {
+      s = reinterpret_cast<uintptr_t>(base) + offs[i];
+      e = s + lens[i];
+      c0 = init ? init[i] : 0u;
+    }
+    const uint32_t crc = ~group_crc_v4(s, e, ~c0, active, lane, (const lds_u32 *)L);
+    if (active && (lane & 15) == 0) out[i] = crc;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kV4Block, 1) void crc32c_msgset_v2_v4_kernel(
+    uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint32_t *__restrict__ caps, uint32_t *__restrict__ out, uint32_t n,
+    const uint32_t *__restrict__ gtab) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[kCrcV4Words];  // the kernel's only LDS: at 0
+  load_tables_v4(L, gtab);
+  const int lane = threadIdx.x & 63;
+  const uint32_t grp = blockIdx.x * kV4Groups + (threadIdx.x >> 4);
+  const uint32_t stride = gridDim.x * kV4Groups;
+  for (uint32_t i0 = blockIdx.x * kV4Groups; i0 < n; i0 += stride) {
+    const uint32_t i = i0 - blockIdx.x * kV4Groups + grp;
+    bool active = i < n;
+    uint8_t *hdr = nullptr;
+    bool bad = false;
+    uintptr_t s = 0, e = 0;
+    if (active) {
+      hdr = base + offs[i];
+      const uint32_t length = be32_at(hdr + 8);  // RD_KAFKAP_MSGSET_V2_OF_Length
+      bad = length < 9u || uint64_t(length) + 12u > caps[i];  // crc_len = Length-4-1-4
+      s = reinterpret_cast<uintptr_t>(hdr) + 21u;
+      e = reinterpret_cast<uintptr_t>(hdr) + 12u + length;
+    }
+    const uint32_t crc = ~group_crc_v4(s, e, ~0u, active && !bad, lane, (const lds_u32 *)L);
+    if (active && (lane & 15) == 0) {
+      if (bad) {
+        out[i] = (MODE == RDK_HIP_V2_CRC_VERIFY) ? 2u : 0u;
+      } else if (MODE == RDK_HIP_V2_CRC_VERIFY) {
+        out[i] = (be32_at(hdr + 17) == crc) ? 0u : 1u;
+      } else {
+        out[i] = crc;
+        if (MODE == RDK_HIP_V2_CRC_FINALIZE) {  // rd_kafka_buf_update_i32 (BE)
+          hdr[17] = uint8_t(crc >> 24);
+          hdr[18] = uint8_t(crc >> 16);
+          hdr[19] = uint8_t(crc >> 8);
+          hdr[20] = uint8_t(crc);
+        }
+      }
+    }
+  }
+}
+
 }  // namespace rdk
 
 // ============================================================ host launchers
 namespace rdk {
 
+// 4 (default): batched kernels on 16-lane groups; RDK_HIP_CRC_V=3 / RDK_HIP_CRC_V1=1 select
+// the earlier per-wave kernels (A/B measurements).  Single long ranges always use v3/v1.
 static int crc_variant() {
-  static const int v = (getenv("RDK_HIP_CRC_V1") && atoi(getenv("RDK_HIP_CRC_V1"))) ? 1 : 3;
+  static const int v = [] {
+    if (getenv("RDK_HIP_CRC_V1") && atoi(getenv("RDK_HIP_CRC_V1"))) return 1;
+    const char *e = getenv("RDK_HIP_CRC_V");
+    return e ? atoi(e) : 4;
+  }();
   return v;
+}
+
+static unsigned crc_grid_v4(uint32_t n) {
+  uint32_t blocks = (n + kV4Groups - 1) / kV4Groups;
+  if (blocks > 256u) blocks = 256u;  // one resident workgroup per CU
+  return blocks ? blocks : 1u;
 }
 
 template <int V> static unsigned crc_grid(uint32_t nwork) {
@@ -466,7 +737,7 @@ int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
     RDK_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_scratch + nchunks), init, 1, s));
     return 0;
   }
-  if (crc_variant() == 3) launch_chunks<3>(c, d_buf, len, init, d_scratch, nchunks, s);
+  if (crc_variant() != 1) launch_chunks<3>(c, d_buf, len, init, d_scratch, nchunks, s);
   else launch_chunks<1>(c, d_buf, len, init, d_scratch, nchunks, s);
   hipLaunchKernelGGL(crc32c_combine_kernel, dim3(1), dim3(64), 0, s, d_scratch, nchunks, len,
                      d_scratch + nchunks, crc_x2n_dev(c->device));
@@ -498,7 +769,10 @@ static void launch_v2(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *
 template <int MODE>
 static void launch_v2_any(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *caps,
                           uint32_t *out, uint32_t n, hipStream_t s) {
-  if (crc_variant() == 3) launch_v2<3, MODE>(c, b, offs, caps, out, n, s);
+  if (crc_variant() == 4)
+    hipLaunchKernelGGL(crc32c_msgset_v2_v4_kernel<MODE>, dim3(crc_grid_v4(n)), dim3(kV4Block), 0,
+                       s, b, offs, caps, out, n, crc_tables_v4_dev(c->device));
+  else if (crc_variant() == 3) launch_v2<3, MODE>(c, b, offs, caps, out, n, s);
   else launch_v2<1, MODE>(c, b, offs, caps, out, n, s);
 }
 
@@ -514,7 +788,11 @@ RDK_API int rdk_hip_crc32c_ranges(const void *d_base, const uint64_t *d_offs,
   if (!n) return RDK_HIP_OK;
   if (!d_base || !d_offs || !d_lens || !d_out) return set_error(RDK_HIP_E_INVAL, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (crc_variant() == 3) launch_ranges<3>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
+  if (crc_variant() == 4)
+    hipLaunchKernelGGL(crc32c_ranges_v4_kernel, dim3(crc_grid_v4(n)), dim3(kV4Block), 0, s,
+                       static_cast<const uint8_t *>(d_base), d_offs, d_lens, d_init, d_out, n,
+                       crc_tables_v4_dev(c->device));
+  else if (crc_variant() == 3) launch_ranges<3>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
   else launch_ranges<1>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
   RDK_HIP_CHECK(hipGetLastError());
   return RDK_HIP_OK;

@@ -42,6 +42,7 @@ constexpr int kMaxDev = 64;
 std::mutex g_mu;
 uint32_t *g_tables[kMaxDev];
 uint32_t *g_tables_v3[kMaxDev];
+uint32_t *g_tables_v4[kMaxDev];
 uint32_t *g_x2n[kMaxDev];
 
 int default_device() {
@@ -54,11 +55,15 @@ int upload_tables(int dev) {
   if (g_tables[dev]) return 0;
   static uint32_t host_tab[kCrcTableWords];
   static uint32_t host_tab2[kCrcV3Words];
+  static uint32_t host_tab4[kCrcV4Words];
   static uint32_t host_x2n[64];
   crc_build_tables(host_tab);
+  crc_build_tables_v4(host_tab4);
   crc_build_tables_v3(host_tab2);
   crc_build_x2n(host_x2n);
-  uint32_t *d = nullptr, *d2 = nullptr, *x = nullptr;
+  uint32_t *d = nullptr, *d2 = nullptr, *d4 = nullptr, *x = nullptr;
+  RDK_HIP_CHECK(hipMalloc(&d4, sizeof host_tab4));
+  RDK_HIP_CHECK(hipMemcpy(d4, host_tab4, sizeof host_tab4, hipMemcpyHostToDevice));
   RDK_HIP_CHECK(hipMalloc(&d, sizeof host_tab));
   RDK_HIP_CHECK(hipMalloc(&d2, sizeof host_tab2));
   RDK_HIP_CHECK(hipMalloc(&x, sizeof host_x2n));
@@ -67,6 +72,7 @@ int upload_tables(int dev) {
   RDK_HIP_CHECK(hipMemcpy(x, host_x2n, sizeof host_x2n, hipMemcpyHostToDevice));
   g_tables[dev] = d;
   g_tables_v3[dev] = d2;
+  g_tables_v4[dev] = d4;
   g_x2n[dev] = x;
   return 0;
 }
@@ -162,6 +168,7 @@ int ensure_desc(Ctx *c, size_t bytes) {
 
 const uint32_t *crc_tables_dev(int device) { return g_tables[device]; }
 const uint32_t *crc_tables_v3_dev(int device) { return g_tables_v3[device]; }
+const uint32_t *crc_tables_v4_dev(int device) { return g_tables_v4[device]; }
 const uint32_t *crc_x2n_dev(int device) { return g_x2n[device]; }
 
 }  // namespace rdk

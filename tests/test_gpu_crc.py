@@ -132,3 +132,55 @@ def test_msgset_v2_large_roundtrip_property(engine):
         b = bytes(buf[i * size:(i + 1) * size].cpu().numpy())
         assert int.from_bytes(b[17:21], "big") == oracle.crc32c(0, b[21:])
     del buf
+
+
+def test_msgset_v2_mixed_lengths(engine, oracle_mod):
+    """Batches of different Length inside one wavefront: the groups of a wave run
+    different step counts (shorter ranges start with zero vectors)."""
+    import torch
+    rnd = random.Random(24)
+    n, size = 300, 16384
+    buf, offs, caps = _batches(engine, n, size, seed=91)
+    lengths = [rnd.choice([9, 10, 40, 60, 61, 100, 255, 256, 1000, 4096, 9999, size - 12])
+               if i % 5 else rnd.randrange(9, size - 11) for i in range(n)]
+    for i, ln in enumerate(lengths):
+        buf[i * size + 8:i * size + 12] = torch.tensor(list(ln.to_bytes(4, "big")),
+                                                       dtype=torch.uint8, device="cuda")
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.msgset_v2_crc(buf, offs, caps, out, engine.V2_CRC_COMPUTE)
+    host = bytes(buf.cpu().numpy())
+    got = out.cpu().numpy().view(np.uint32)
+    for i in range(n):
+        b = host[i * size:(i + 1) * size]
+        assert got[i] == oracle_mod.crc32c(0, b[21:12 + lengths[i]]), (i, lengths[i])
+
+
+def test_ranges_far_apart(engine, oracle_mod):
+    """Ranges of one wavefront more than 2 GiB apart take separate passes (each
+    pass reads through one 31-bit buffer window)."""
+    import torch
+    span = (2 << 30) + (300 << 20)
+    dev = torch.empty(span, dtype=torch.uint8, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    lo_o, hi_o, mid_o = 4096 + 3, span - (1 << 20), (1 << 30) + 77
+    for o in (lo_o, hi_o, mid_o):
+        dev[o:o + (1 << 19)] = torch.randint(0, 256, (1 << 19,), dtype=torch.uint8,
+                                             device="cuda", generator=g)
+    rnd = random.Random(25)
+    offs, lens = [], []
+    for i in range(256):
+        base = (lo_o, hi_o, mid_o)[rnd.randrange(3)]
+        ln = rnd.choice([70, 1000, 16363, 100000])
+        offs.append(base + rnd.randrange(0, (1 << 19) - ln)); lens.append(ln)
+    to = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    tl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    out = torch.zeros(len(offs), dtype=torch.int32, device="cuda")
+    engine.crc32c_ranges(dev, to, tl, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    windows = {o: bytes(dev[o:o + (1 << 19)].cpu().numpy()) for o in (lo_o, hi_o, mid_o)}
+    for i, (o, ln) in enumerate(zip(offs, lens)):
+        base = max(b for b in windows if b <= o)
+        data = windows[base][o - base:o - base + ln]
+        assert got[i] == oracle_mod.crc32c(0, data), (i, o, ln)
+    del dev

@@ -29,7 +29,8 @@ except Exception:  # pragma: no cover - torch is always installed here
 from . import workload  # noqa: E402,F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librdkafka_hip.so")
+# RDK_HIP_LIB: an alternative build of the same library (kernel A/B experiments)
+LIB_PATH = os.environ.get("RDK_HIP_LIB") or os.path.join(_HERE, "librdkafka_hip.so")
 
 RESP_ERR_NO_ERROR = 0
 RESP_ERR__BAD_MSG = -199

@@ -299,7 +299,13 @@ __device__ __attribute__((always_inline)) uint32_t wave_crc_v3(uintptr_t s, uint
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr uint32_t kNoLoad = 0x80000000u;  // buffer offset past num_records: reads 0
 constexpr uint32_t kV4Span = 0x7f000000u;  // ranges of one pass lie within this of its base
-constexpr int kV4Prefetch = 8;             // 256-byte group steps in flight per lane
+#ifndef RDK_V4_AUX
+#define RDK_V4_AUX 2  // nt: streamed once
+#endif
+#ifndef RDK_V4_PREFETCH
+#define RDK_V4_PREFETCH 4
+#endif
+constexpr int kV4Prefetch = RDK_V4_PREFETCH;  // group steps in flight per lane (x kV4Vecs loads)
 
 // selector: byte 0 <- C byte t (4c | 0x80t), byte 1 <- register byte q, byte 2 <- C byte 2
 // (0x01) for the upper half, else 0; byte 3 <- 0
@@ -327,6 +333,12 @@ __device__ __forceinline__ uint32_t v4_step(const lds_u32 *Lb, uint32_t r, uint3
 __device__ __forceinline__ uint32_t v4_z4(const lds_u32 *Lb, uint32_t x) {
   return lds4(Lb, (x & 0xffu) << 2, kV4Z4) ^ lds4(Lb, ((x >> 8) & 0xffu) << 2, kV4Z4 + 1024) ^
          lds4(Lb, ((x >> 16) & 0xffu) << 2, kV4Z4 + 2048) ^ lds4(Lb, (x >> 24) << 2, kV4Z4 + 3072);
+}
+
+__device__ __forceinline__ uint32_t v4_z256(const lds_u32 *Lb, uint32_t x) {
+  return lds4(Lb, (x & 0xffu) << 2, kV4Z256) ^ lds4(Lb, ((x >> 8) & 0xffu) << 2, kV4Z256 + 1024) ^
+         lds4(Lb, ((x >> 16) & 0xffu) << 2, kV4Z256 + 2048) ^
+         lds4(Lb, (x >> 24) << 2, kV4Z256 + 3072);
 }
 
 __device__ __forceinline__ uint32_t v4_fin(const lds_u32 *Lb, uint32_t x, uint32_t lc4) {
@@ -376,8 +388,10 @@ __device__ __attribute__((always_inline)) uint32_t group_crc_v4(uintptr_t s, uin
     return c;
   }
   const uintptr_t A = s & ~uintptr_t(15), B = e & ~uintptr_t(15);
-  const uint32_t K = big ? uint32_t(((B - A) >> 4) + 15u) >> 4 : 0u;  // 256-byte steps
-  uint32_t F0 = 0, F1 = 0, F2 = 0, F3 = 0;
+  constexpr int NV = kV4Vecs;
+  constexpr int P = kV4Prefetch;
+  const uint32_t K = big ? uint32_t(((B - A) >> 4) + 16u * NV - 1u) / (16u * NV) : 0u;  // steps
+  uint32_t R[NV][4] = {};  // Horner registers; a lane only steps them in its own pass
   // groups still to do: one bit per group leader lane
   uint64_t todo = __builtin_amdgcn_ballot_w64(big && l == 0);
   while (todo) {
@@ -395,73 +409,85 @@ __device__ __attribute__((always_inline)) uint32_t group_crc_v4(uintptr_t s, uin
       const uint32_t k = __builtin_amdgcn_readlane(K, int(__builtin_ctzll(t)));
       Kmax = k > Kmax ? k : Kmax;
     }
+    // whole blocks of P steps: extra leading steps lie before every range and read zeros,
+    // which leave a raw CRC register unchanged
+    Kmax = (Kmax + P - 1) / P * P;
     const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(sb), 0,
                                                         int(kNoLoad), 0x00020000);
-    // lane offsets relative to sb: vector k at o0 + 256k; below lowA (before the range,
-    // including the shorter ranges' leading steps) the load is parked and reads 0
-    // (lanes outside the pass: INT32_MIN, so that every offset stays >= kNoLoad)
+    // lane offsets relative to sb: vector v of step k at o0 + kV4Step*k + 256v; below
+    // lowA (before the range, including the shorter ranges' leading steps) the load is
+    // parked and reads 0 (lanes outside the pass: o0 = INT32_MIN, every offset >= kNoLoad)
     const int32_t o0 =
-        inpass ? int32_t(uint32_t(B - sb) - kV4Stride * Kmax + 16u * l) : int32_t(kNoLoad);
+        inpass ? int32_t(uint32_t(B - sb) - kV4Step * Kmax + 16u * l) : int32_t(kNoLoad);
     const int32_t lowA = inpass ? int32_t(uint32_t(A - sb)) : 0x7fffffff;
     const uint32_t srel = uint32_t(s - sb);
-    auto off = [&](uint32_t k) -> uint32_t {
-      const int32_t o = o0 + int32_t(kV4Stride * k);
+    auto voff = [&](uint32_t k, int v) -> int32_t { return o0 + int32_t(kV4Step * k + 256 * v); };
+    auto off = [&](uint32_t k, int v) -> uint32_t {
+      const int32_t o = voff(k, v);
       return (k < Kmax && o >= lowA) ? uint32_t(o) : kNoLoad;
     };
     // last step holding a head vector ([A, A+32) of some range in the pass): blocks after it
     // load unconditionally and skip the head check
     uint32_t khead = 0;
     {
-      const int32_t kl = inpass ? (lowA + 31 - o0) >> 8 : 0;  // per group leader (l = 0)
+      const int32_t kl = inpass ? (lowA + 31 - o0) / kV4Step : 0;  // per group leader (l = 0)
       for (uint64_t t = pm; t; t &= t - 1) {
         const int32_t k = __builtin_amdgcn_readlane(kl, int(__builtin_ctzll(t)));
         khead = uint32_t(k) > khead ? uint32_t(k) : khead;
       }
     }
-    uint32_t R0 = 0, R1 = 0, R2 = 0, R3 = 0;
-    u32x4 buf[kV4Prefetch];
+    u32x4 buf[P][NV];
 #pragma unroll
-    for (int j = 0; j < kV4Prefetch; ++j)
-      buf[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off(uint32_t(j)), 0, 2);
-    // one block = kV4Prefetch steps; CHK: steps may hold heads, loads may fall outside
+    for (int j = 0; j < P; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        buf[j][v] = __builtin_amdgcn_raw_buffer_load_b128(rs, off(uint32_t(j), v), 0, RDK_V4_AUX);
+    // one block = P steps; CHK: its steps may hold heads and its loads may fall outside
+    // the ranges.  Each slot is refilled right after it is consumed, so the load ring keeps
+    // its registers across blocks and loops (no drains).
     auto block = [&](uint32_t k0, auto chk) __attribute__((always_inline)) {
       constexpr bool CHK = decltype(chk)::value;
 #pragma unroll
-      for (int j = 0; j < kV4Prefetch; ++j) {
+      for (int j = 0; j < P; ++j) {
         const uint32_t k = k0 + uint32_t(j);
-        if (!CHK || k < Kmax) {
-          u32x4 w = buf[j];
-          const uint32_t kn = k + kV4Prefetch;
-          buf[j] = __builtin_amdgcn_raw_buffer_load_b128(
-              rs, CHK ? off(kn) : uint32_t(o0 + int32_t(kV4Stride * kn)), 0, 2);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          u32x4 w = buf[j][v];
           if (CHK) {
-            const int32_t o = o0 + int32_t(kV4Stride * k);
-            if (o >= lowA && o < lowA + 32) {  // head: zero bytes before s, inject ninit
-              const uintptr_t d = uintptr_t(uint32_t(o));
+            const int32_t oc = voff(k, v);
+            if (oc >= lowA && oc < lowA + 32) {  // head: zero bytes before s, inject ninit
+              const uintptr_t d = uintptr_t(uint32_t(oc));
               w.x = head_fix(w.x, d, srel, ninit);
               w.y = head_fix(w.y, d + 4, srel, ninit);
               w.z = head_fix(w.z, d + 8, srel, ninit);
               w.w = head_fix(w.w, d + 12, srel, ninit);
             }
           }
-          R0 = v4_step(Lb, R0, w.x, C);
-          R1 = v4_step(Lb, R1, w.y, C);
-          R2 = v4_step(Lb, R2, w.z, C);
-          R3 = v4_step(Lb, R3, w.w, C);
+          R[v][0] = v4_step(Lb, R[v][0], w.x, C);
+          R[v][1] = v4_step(Lb, R[v][1], w.y, C);
+          R[v][2] = v4_step(Lb, R[v][2], w.z, C);
+          R[v][3] = v4_step(Lb, R[v][3], w.w, C);
+          const uint32_t kn = k + P;
+          buf[j][v] = __builtin_amdgcn_raw_buffer_load_b128(
+              rs, CHK ? off(kn, v) : uint32_t(voff(kn, v)), 0, RDK_V4_AUX);
         }
       }
     };
-    for (uint32_t k0 = 0; k0 < Kmax; k0 += kV4Prefetch) {
-      if (k0 > khead && k0 + 2 * kV4Prefetch <= Kmax) block(k0, std::false_type{});
-      else block(k0, std::true_type{});
+    if (inpass) {
+      uint32_t k0 = 0;
+      for (; k0 < Kmax && (k0 <= khead || k0 + 2 * P > Kmax); k0 += P)
+        block(k0, std::true_type{});
+      for (; k0 + 2 * P <= Kmax; k0 += P) block(k0, std::false_type{});
+      for (; k0 < Kmax; k0 += P) block(k0, std::true_type{});
     }
-    F0 ^= R0;  // lanes outside the pass kept R = 0
-    F1 ^= R1;
-    F2 ^= R2;
-    F3 ^= R3;
   }
-  // combine the four dword streams, place lane l, reduce the group
-  uint32_t r = v4_z4(Lb, v4_z4(Lb, v4_z4(Lb, F0) ^ F1) ^ F2) ^ F3;
+  // combine each vector's four dword streams, then the vectors, place lane l, reduce
+  uint32_t r = 0;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const uint32_t x = v4_z4(Lb, v4_z4(Lb, v4_z4(Lb, R[v][0]) ^ R[v][1]) ^ R[v][2]) ^ R[v][3];
+    r = v ? v4_z256(Lb, r) ^ x : x;
+  }
   r = row_xor(v4_fin(Lb, r, lc4));
   // fold the <16-byte tail [B, e) byte by byte (crc32c.c:131)
   if (big) {

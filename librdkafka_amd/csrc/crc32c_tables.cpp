@@ -93,7 +93,7 @@ void crc_build_tables_v3(uint32_t *out) {
 void crc_build_tables_v4(uint32_t *out) {
   std::memset(out, 0, size_t(kCrcV4Bytes));
   uint32_t op[32];
-  crc_zeros_operator(op, size_t(kV4Stride));
+  crc_zeros_operator(op, size_t(kV4Step));
   for (int q = 0; q < 4; ++q)
     for (uint32_t b = 0; b < 256; ++b) {
       const uint32_t v = crc_gf2_times(op, b << (8 * q));
@@ -101,7 +101,7 @@ void crc_build_tables_v4(uint32_t *out) {
         out[((q >> 1) * 0x10000 + int(b) * 256 + (q & 1) * 128 + c * 4) / 4] = v;
     }
   for (int l = 0; l < 16; ++l) {  // Fin: lane l of a group is 256-16l-12 bytes before the end
-    crc_zeros_operator(op, size_t(kV4Stride - 16 * l - 12));
+    crc_zeros_operator(op, size_t(256 - 16 * l - 12));
     for (int i = 0; i < 8; ++i)
       for (uint32_t n = 0; n < 16; ++n) {
         const uint32_t v = crc_gf2_times(op, n << (4 * i));
@@ -112,6 +112,10 @@ void crc_build_tables_v4(uint32_t *out) {
   for (int q = 0; q < 4; ++q)
     for (uint32_t b = 0; b < 256; ++b)
       out[(kV4Z4 + q * 1024) / 4 + int(b)] = crc_gf2_times(op, b << (8 * q));
+  crc_zeros_operator(op, 256);
+  for (int q = 0; q < 4; ++q)
+    for (uint32_t b = 0; b < 256; ++b)
+      out[(kV4Z256 + q * 1024) / 4 + int(b)] = crc_gf2_times(op, b << (8 * q));
 }
 
 // x2n[k] = x^(2^k) mod P in reflected form (bit 31 = x^0), for the

@@ -57,23 +57,30 @@ void crc_build_tables_v3(uint32_t *out /* kCrcV3Words */);
 void crc_build_x2n(uint32_t *out /* 64 */);
 
 // ---- v4 image (batched ranges / MsgVersion 2 kernels): 16-lane groups, byte tables
-// A 16-lane group CRCs one range: lane l owns the 16-byte vectors at V + 256k + 16l and runs
-// four Horner streams, one per dword slot j, all with the same map Z_256 ("advance 256
-// zero bytes"): R_j = Z_256(R_j) ^ w_j.  Z_256 is 4 byte tables (one per input byte q),
+// A 16-lane group CRCs one range.  Per step the group reads kV4Vecs x 256 contiguous bytes:
+// lane l owns the 16-byte vectors at V + kV4Step*k + 256v + 16l (v < kV4Vecs) and runs
+// 4*kV4Vecs Horner streams, one per dword slot, all with the same map Z_kV4Step ("advance
+// kV4Step zero bytes"): R = Z(R) ^ w.  Z is 4 byte tables (one per input byte q),
 // 32-fold replicated (copy c = lane % 32 -> bank c, conflict-free), in two 64 KiB halves
 // h = q >> 1 with the two tables t = q & 1 of a half interleaved per entry:
 //   address = h*0x10000 + b*256 + t*128 + 4c
 // so that ONE v_perm_b32 builds an address from the register byte b and a per-lane
-// constant holding 4c, 4c|0x80 and 0x01 (kernel: v4_sel).  End of a range: the four
-// streams combine through Z_4 (unreplicated byte tables; T0 = its table 3), then lane l's
-// register is advanced by Z_{244-16l} -- "Fin", nibble tables whose copy c holds the map
-// of group lane c % 16 -- and the 16 lanes xor-reduce inside their DPP row.
-constexpr int kV4Stride = 256;                  // bytes between a group lane's vectors
+// constant holding 4c, 4c|0x80 and 0x01 (kernel: v4_sel).  End of a range: each vector's
+// four streams combine through Z_4, the vectors through Z_256 (both unreplicated byte
+// tables; T0 = Z_4's table 3), then lane l's register is advanced by Z_{244-16l} -- "Fin",
+// nibble tables whose copy c holds the map of group lane c % 16 -- and the 16 lanes
+// xor-reduce inside their DPP row.
+#ifndef RDK_V4_VECS
+#define RDK_V4_VECS 2
+#endif
+constexpr int kV4Vecs = RDK_V4_VECS;            // 16-byte vectors per lane per step
+constexpr int kV4Step = 256 * kV4Vecs;          // bytes between a lane's steps
 constexpr int kV4Main = 0;
 constexpr int kV4Fin = 0x20000;                 // nibble i at +2048*i, entry n at +128*n
 constexpr int kV4Z4 = 0x24000;                  // byte table q at +1024*q
 constexpr int kV4T0 = kV4Z4 + 3 * 1024;
-constexpr int kCrcV4Bytes = kV4Z4 + 4 * 1024;   // 151552 B = 148 KiB (one workgroup per CU)
+constexpr int kV4Z256 = 0x25000;                // byte table q at +1024*q
+constexpr int kCrcV4Bytes = kV4Z256 + 4 * 1024; // 155648 B = 152 KiB (one workgroup per CU)
 constexpr int kCrcV4Words = kCrcV4Bytes / 4;
 void crc_build_tables_v4(uint32_t *out /* kCrcV4Words */);
 

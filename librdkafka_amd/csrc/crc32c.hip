@@ -323,6 +323,9 @@ template <int Q> constexpr uint32_t v4_sel() {
 }
 
 __device__ __forceinline__ uint32_t v4_step(const lds_u32 *Lb, uint32_t r, uint32_t w, uint32_t C) {
+#if defined(RDK_V4_ABL) && RDK_V4_ABL == 2  // timing ablation only: no table lookups
+  return xor3(r, w, C);
+#endif
   const uint32_t a = lds4(Lb, __builtin_amdgcn_perm(r, C, v4_sel<0>()), 0);
   const uint32_t b = lds4(Lb, __builtin_amdgcn_perm(r, C, v4_sel<1>()), 0);
   const uint32_t c = lds4(Lb, __builtin_amdgcn_perm(r, C, v4_sel<2>()), 0);
@@ -376,7 +379,7 @@ __device__ __attribute__((always_inline)) uint32_t group_crc_v4(uintptr_t s, uin
                                                                uint32_t ninit, bool active,
                                                                int lane, const lds_u32 *Lb) {
   typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
-  const uint32_t l = uint32_t(lane) & 15u;
+  const uint32_t l = uint32_t(lane) & uint32_t(kV4Lanes - 1);
   const uint32_t lc4 = (uint32_t(lane) & 31u) << 2;
   const uint32_t C = lc4 | ((lc4 | 0x80u) << 8) | (1u << 16);
   const size_t len = active ? e - s : 0;
@@ -390,7 +393,8 @@ __device__ __attribute__((always_inline)) uint32_t group_crc_v4(uintptr_t s, uin
   const uintptr_t A = s & ~uintptr_t(15), B = e & ~uintptr_t(15);
   constexpr int NV = kV4Vecs;
   constexpr int P = kV4Prefetch;
-  const uint32_t K = big ? uint32_t(((B - A) >> 4) + 16u * NV - 1u) / (16u * NV) : 0u;  // steps
+  constexpr uint32_t VPS = uint32_t(kV4Lanes * NV);  // group vectors per step
+  const uint32_t K = big ? uint32_t(((B - A) >> 4) + VPS - 1u) / VPS : 0u;  // steps
   uint32_t R[NV][4] = {};  // Horner registers; a lane only steps them in its own pass
   // groups still to do: one bit per group leader lane
   uint64_t todo = __builtin_amdgcn_ballot_w64(big && l == 0);
@@ -401,7 +405,7 @@ __device__ __attribute__((always_inline)) uint32_t group_crc_v4(uintptr_t s, uin
       const uintptr_t a = rdlane64(A, int(__builtin_ctzll(t)));
       sb = a < sb ? a : sb;
     }
-    const bool inpass = big && ((todo >> (lane & 48)) & 1u) && B - sb < kV4Span;
+    const bool inpass = big && ((todo >> (lane & (64 - kV4Lanes))) & 1u) && B - sb < kV4Span;
     const uint64_t pm = __builtin_amdgcn_ballot_w64(inpass && l == 0);
     todo &= ~pm;
     uint32_t Kmax = 0;
@@ -421,7 +425,7 @@ __device__ __attribute__((always_inline)) uint32_t group_crc_v4(uintptr_t s, uin
         inpass ? int32_t(uint32_t(B - sb) - kV4Step * Kmax + 16u * l) : int32_t(kNoLoad);
     const int32_t lowA = inpass ? int32_t(uint32_t(A - sb)) : 0x7fffffff;
     const uint32_t srel = uint32_t(s - sb);
-    auto voff = [&](uint32_t k, int v) -> int32_t { return o0 + int32_t(kV4Step * k + 256 * v); };
+    auto voff = [&](uint32_t k, int v) -> int32_t { return o0 + int32_t(kV4Step * k + kV4Row * v); };
     auto off = [&](uint32_t k, int v) -> uint32_t {
       const int32_t o = voff(k, v);
       return (k < Kmax && o >= lowA) ? uint32_t(o) : kNoLoad;
@@ -483,12 +487,16 @@ __device__ __attribute__((always_inline)) uint32_t group_crc_v4(uintptr_t s, uin
   }
   // combine each vector's four dword streams, then the vectors, place lane l, reduce
   uint32_t r = 0;
+#if defined(RDK_V4_ABL) && RDK_V4_ABL == 1  // timing ablation only: skip the combine
+  if (big) return R[0][0] ^ R[0][1] ^ R[NV - 1][2] ^ R[NV - 1][3];
+#endif
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const uint32_t x = v4_z4(Lb, v4_z4(Lb, v4_z4(Lb, R[v][0]) ^ R[v][1]) ^ R[v][2]) ^ R[v][3];
     r = v ? v4_z256(Lb, r) ^ x : x;
   }
   r = row_xor(v4_fin(Lb, r, lc4));
+  if (kV4Lanes == 32) r ^= __builtin_amdgcn_ds_swizzle(r, 0x401f);  // xor lane 16
   // fold the <16-byte tail [B, e) byte by byte (crc32c.c:131)
   if (big) {
     gbl_u8 *p = (gbl_u8 *)B;
@@ -635,7 +643,7 @@ __global__ __launch_bounds__(crc_block<V>(), 8) void crc32c_msgset_v2_kernel(
 // ---- v4 kernels: 16 waves x 4 groups = 64 ranges per workgroup round; the
 // 148 KiB table image allows one workgroup per CU
 constexpr int kV4Block = 1024;
-constexpr int kV4Groups = kV4Block / 16;
+constexpr int kV4Groups = kV4Block / kV4Lanes;
 
 __device__ __forceinline__ void load_tables_v4(uint32_t *L, const uint32_t *g) {
   const uint4 *src = reinterpret_cast<const uint4 *>(g);
@@ -651,7 +659,7 @@ __global__ __launch_bounds__(kV4Block, 1) void crc32c_ranges_v4_kernel(
   __shared__ __attribute__((aligned(16))) uint32_t L[kCrcV4Words];  // the kernel's only LDS: at 0
   load_tables_v4(L, gtab);
   const int lane = threadIdx.x & 63;
-  const uint32_t grp = blockIdx.x * kV4Groups + (threadIdx.x >> 4);
+  const uint32_t grp = blockIdx.x * kV4Groups + (threadIdx.x / kV4Lanes);
   const uint32_t stride = gridDim.x * kV4Groups;
   // every wave runs the same number of rounds (uniform trip count)
   for (uint32_t i0 = blockIdx.x * kV4Groups; i0 < n; i0 += stride) {
@@ -665,7 +673,7 @@ __global__ __launch_bounds__(kV4Block, 1) void crc32c_ranges_v4_kernel(
       c0 = init ? init[i] : 0u;
     }
     const uint32_t crc = ~group_crc_v4(s, e, ~c0, active, lane, (const lds_u32 *)L);
-    if (active && (lane & 15) == 0) out[i] = crc;
+    if (active && (lane & (kV4Lanes - 1)) == 0) out[i] = crc;
   }
 }
 
@@ -677,23 +685,35 @@ __global__ __launch_bounds__(kV4Block, 1) void crc32c_msgset_v2_v4_kernel(
   __shared__ __attribute__((aligned(16))) uint32_t L[kCrcV4Words];  // the kernel's only LDS: at 0
   load_tables_v4(L, gtab);
   const int lane = threadIdx.x & 63;
-  const uint32_t grp = blockIdx.x * kV4Groups + (threadIdx.x >> 4);
+  const uint32_t grp = blockIdx.x * kV4Groups + (threadIdx.x / kV4Lanes);
   const uint32_t stride = gridDim.x * kV4Groups;
-  for (uint32_t i0 = blockIdx.x * kV4Groups; i0 < n; i0 += stride) {
-    const uint32_t i = i0 - blockIdx.x * kV4Groups + grp;
-    bool active = i < n;
-    uint8_t *hdr = nullptr;
-    bool bad = false;
-    uintptr_t s = 0, e = 0;
-    if (active) {
-      hdr = base + offs[i];
-      const uint32_t length = be32_at(hdr + 8);  // RD_KAFKAP_MSGSET_V2_OF_Length
-      bad = length < 9u || uint64_t(length) + 12u > caps[i];  // crc_len = Length-4-1-4
-      s = reinterpret_cast<uintptr_t>(hdr) + 21u;
-      e = reinterpret_cast<uintptr_t>(hdr) + 12u + length;
-    }
+  // batch metadata is software-pipelined over the rounds: the offset two rounds ahead and
+  // the Length word / capacity one round ahead are loaded before this round's CRC, so no
+  // round starts with a chain of dependent loads (indices clamped: always valid addresses)
+  typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
+  auto clampi = [&](uint32_t j) { return j < n ? j : n - 1u; };
+  auto len_word = [&](uint64_t o) {
+    gbl_u8 *p = (gbl_u8 *)(base + o + 8);  // RD_KAFKAP_MSGSET_V2_OF_Length (big-endian)
+    return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
+  };
+  uint32_t i = grp;
+  uint64_t o_nx = offs[clampi(i)];
+  uint32_t len_nx = len_word(o_nx), cap_nx = caps[clampi(i)];
+  uint64_t o_nx2 = offs[clampi(i + stride)];
+  for (uint32_t i0 = blockIdx.x * kV4Groups; i0 < n; i0 += stride, i += stride) {
+    const bool active = i < n;
+    const uint64_t o = o_nx;
+    const uint32_t length = len_nx, cap = cap_nx;
+    o_nx = o_nx2;
+    len_nx = len_word(o_nx);
+    cap_nx = caps[clampi(i + stride)];
+    o_nx2 = offs[clampi(i + 2 * stride)];
+    uint8_t *hdr = base + o;
+    const bool bad = length < 9u || uint64_t(length) + 12u > cap;  // crc_len = Length-4-1-4
+    const uintptr_t s = reinterpret_cast<uintptr_t>(hdr) + 21u;
+    const uintptr_t e = reinterpret_cast<uintptr_t>(hdr) + 12u + length;
     const uint32_t crc = ~group_crc_v4(s, e, ~0u, active && !bad, lane, (const lds_u32 *)L);
-    if (active && (lane & 15) == 0) {
+    if (active && (lane & (kV4Lanes - 1)) == 0) {
       if (bad) {
         out[i] = (MODE == RDK_HIP_V2_CRC_VERIFY) ? 2u : 0u;
       } else if (MODE == RDK_HIP_V2_CRC_VERIFY) {

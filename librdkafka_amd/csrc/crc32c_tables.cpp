@@ -100,19 +100,19 @@ void crc_build_tables_v4(uint32_t *out) {
       for (int c = 0; c < 32; ++c)
         out[((q >> 1) * 0x10000 + int(b) * 256 + (q & 1) * 128 + c * 4) / 4] = v;
     }
-  for (int l = 0; l < 16; ++l) {  // Fin: lane l of a group is 256-16l-12 bytes before the end
-    crc_zeros_operator(op, size_t(256 - 16 * l - 12));
+  for (int l = 0; l < kV4Lanes; ++l) {  // Fin: group lane l's last dword stream ends
+    crc_zeros_operator(op, size_t(kV4Row - 16 * l - 12));  // kV4Row-16l-12 bytes early
     for (int i = 0; i < 8; ++i)
       for (uint32_t n = 0; n < 16; ++n) {
         const uint32_t v = crc_gf2_times(op, n << (4 * i));
-        for (int c = l; c < 32; c += 16) out[(kV4Fin + i * 2048 + int(n) * 128 + c * 4) / 4] = v;
+        for (int c = l; c < 32; c += kV4Lanes) out[(kV4Fin + i * 2048 + int(n) * 128 + c * 4) / 4] = v;
       }
   }
   crc_zeros_operator(op, 4);
   for (int q = 0; q < 4; ++q)
     for (uint32_t b = 0; b < 256; ++b)
       out[(kV4Z4 + q * 1024) / 4 + int(b)] = crc_gf2_times(op, b << (8 * q));
-  crc_zeros_operator(op, 256);
+  crc_zeros_operator(op, size_t(kV4Row));
   for (int q = 0; q < 4; ++q)
     for (uint32_t b = 0; b < 256; ++b)
       out[(kV4Z256 + q * 1024) / 4 + int(b)] = crc_gf2_times(op, b << (8 * q));

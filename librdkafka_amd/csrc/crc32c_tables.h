@@ -70,16 +70,21 @@ void crc_build_x2n(uint32_t *out /* 64 */);
 // tables; T0 = Z_4's table 3), then lane l's register is advanced by Z_{244-16l} -- "Fin",
 // nibble tables whose copy c holds the map of group lane c % 16 -- and the 16 lanes
 // xor-reduce inside their DPP row.
+#ifndef RDK_V4_LANES
+#define RDK_V4_LANES 16
+#endif
+constexpr int kV4Lanes = RDK_V4_LANES;          // lanes per group (one range): 16 or 32
+constexpr int kV4Row = 16 * kV4Lanes;           // bytes of one group vector row
 #ifndef RDK_V4_VECS
 #define RDK_V4_VECS 2
 #endif
 constexpr int kV4Vecs = RDK_V4_VECS;            // 16-byte vectors per lane per step
-constexpr int kV4Step = 256 * kV4Vecs;          // bytes between a lane's steps
+constexpr int kV4Step = kV4Row * kV4Vecs;       // bytes between a lane's steps
 constexpr int kV4Main = 0;
 constexpr int kV4Fin = 0x20000;                 // nibble i at +2048*i, entry n at +128*n
 constexpr int kV4Z4 = 0x24000;                  // byte table q at +1024*q
 constexpr int kV4T0 = kV4Z4 + 3 * 1024;
-constexpr int kV4Z256 = 0x25000;                // byte table q at +1024*q
+constexpr int kV4Z256 = 0x25000;                // Z_kV4Row: byte table q at +1024*q
 constexpr int kCrcV4Bytes = kV4Z256 + 4 * 1024; // 155648 B = 152 KiB (one workgroup per CU)
 constexpr int kCrcV4Words = kCrcV4Bytes / 4;
 void crc_build_tables_v4(uint32_t *out /* kCrcV4Words */);

@@ -186,6 +186,44 @@ int rdk_hip_producer_flush(rdk_hip_producer_t *p);
 int rdk_hip_producer_poll(rdk_hip_producer_t *p, rdk_hip_batch_t *out, int max, int block);
 void rdk_hip_producer_destroy(rdk_hip_producer_t *p);
 
+/* ---- MsgVersion 2 record serialisation --------------------
+ * For device-resident messages, replaces
+ *   rd_kafka_msgset_writer_write_MessageSet_v2_header  rdkafka_msgset_writer.c:352-403
+ *   rd_kafka_msgset_writer_write_msg_v2                 rdkafka_msgset_writer.c:652-754
+ *   rd_kafka_msgset_writer_finalize_MessageSet_v2_header rdkafka_msgset_writer.c:1251-1295
+ * with write_msgq's batch semantics (:804-902): OffsetDelta = index in the batch,
+ * TimestampDelta against the batch's first message, MaxTimestamp starting at 0.
+ * Output: uncompressed batches (61-byte header + records), CRC optional. */
+typedef struct rdk_hip_msgs_s {     /* all device pointers, one entry per message */
+  const uint8_t *arena;             /* key / value / header bytes */
+  const int64_t *timestamp;         /* rkm_timestamp */
+  const uint64_t *key_off;
+  const int32_t *key_len;           /* -1: null key (RD_KAFKAP_BYTES_LEN_NULL) */
+  const uint64_t *value_off;
+  const int32_t *value_len;         /* -1: null value */
+  const uint64_t *headers_off;      /* headers already in wire form (:558-568) */
+  const uint32_t *headers_len;
+  const int32_t *header_count;      /* NULL: no message has headers */
+} rdk_hip_msgs_t;
+typedef struct rdk_hip_v2_batch_s { /* one MessageSet: messages [first_msg, +msg_count) */
+  uint32_t first_msg, msg_count;
+  int64_t producer_id;              /* msetw_pid.id (:392) */
+  int32_t base_sequence;            /* msetw_batch->first_seq (:1289), -1 if none */
+  int16_t producer_epoch;           /* (:395) */
+  int16_t attributes;               /* codec bits etc. (:1271) */
+} rdk_hip_v2_batch_t;
+/* Pass 1: d_rec_offs[m] = offset of message m's record from its batch start
+ * (header included), d_batch_sizes[b] = 61 + records bytes. */
+int rdk_hip_msgset_v2_sizes(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *d_batches,
+                            uint32_t n_batches, uint32_t *d_rec_offs, uint32_t *d_batch_sizes,
+                            void *stream);
+/* Pass 2: batch b written at d_out + d_out_offs[b] (d_batch_sizes[b] bytes); with d_crc
+ * the CRC32C is stored at offset 17 as calc_crc_v2 does (:1229-1246) and in d_crc[b]. */
+int rdk_hip_msgset_v2_write(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *d_batches,
+                            uint32_t n_batches, const uint32_t *d_rec_offs,
+                            const uint32_t *d_batch_sizes, const uint64_t *d_out_offs,
+                            uint8_t *d_out, uint32_t *d_crc, void *stream);
+
 /* Deterministic synthetic workloads generated on the device (bench/tests).
  * v2 batches: n batches of `batch_size` bytes at i*batch_size: a valid 61-byte
  * v2 header (Magic 2, Length = batch_size-12, RecordCount) followed by

@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import subprocess
+import numpy as np
 
 try:  # share torch's HIP runtime (same SONAME) when torch is present
     import torch  # noqa: F401
@@ -48,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "rdk_hip_lz4f_compress", "rdk_hip_lz4f_compress_fast", "rdk_hip_lz4f_decompress",
     "rdk_hip_gen_v2_batches", "rdk_hip_producer_new", "rdk_hip_producer_produce",
     "rdk_hip_producer_flush", "rdk_hip_producer_poll", "rdk_hip_producer_destroy",
-    "rdk_hip_gen_json",
+    "rdk_hip_gen_json", "rdk_hip_msgset_v2_sizes", "rdk_hip_msgset_v2_write",
 )
 
 
@@ -114,8 +115,25 @@ def lib():
     L.rdk_hip_gen_v2_batches.argtypes = [vp, u32, u32, C.c_uint64, vp]
     L.rdk_hip_gen_json.restype = None
     L.rdk_hip_gen_json.argtypes = [vp, sz, u32]
+    L.rdk_hip_msgset_v2_sizes.restype = i32
+    L.rdk_hip_msgset_v2_sizes.argtypes = [C.POINTER(_Msgs), vp, u32, vp, vp, vp]
+    L.rdk_hip_msgset_v2_write.restype = i32
+    L.rdk_hip_msgset_v2_write.argtypes = [C.POINTER(_Msgs), vp, u32, vp, vp, vp, vp, vp, vp]
     _lib = L
     return L
+
+
+class _Msgs(C.Structure):
+    """rdk_hip_msgs_t (include/librdkafka_hip.h): device pointers, one entry per message."""
+    _fields_ = [(n, C.c_void_p) for n in ("arena", "timestamp", "key_off", "key_len", "value_off",
+                                          "value_len", "headers_off", "headers_len",
+                                          "header_count")]
+
+
+# rdk_hip_v2_batch_t
+V2_BATCH_DTYPE = np.dtype([("first_msg", "<u4"), ("msg_count", "<u4"), ("producer_id", "<i8"),
+                           ("base_sequence", "<i4"), ("producer_epoch", "<i2"),
+                           ("attributes", "<i2")])
 
 
 def _check(rc: int, what: str) -> None:
@@ -368,3 +386,33 @@ def gen_json(n: int, seed: int = 42) -> bytes:
     b = C.create_string_buffer(max(1, n))
     lib().rdk_hip_gen_json(b, n, seed)
     return b.raw[:n]
+
+
+def msgset_v2_build(msgs: dict, batches: np.ndarray, crc: bool = True, stream=None):
+    """MsgVersion 2 record serialisation on the device (rdkafka_msgset_writer.c:352-403,
+    :652-754, :1251-1295).  `msgs`: cuda tensors arena (u8), ts (i64), key_off (i64),
+    key_len (i32), val_off (i64), val_len (i32) and optionally hdr_off (i64),
+    hdr_len (i32), hdr_cnt (i32); `batches`: numpy array of V2_BATCH_DTYPE.
+    Returns (out u8 tensor, out_offs i64 tensor, batch_sizes i32 tensor, crcs i32 tensor
+    or None)."""
+    n = len(batches)
+    dev = msgs["arena"].device
+    m = _Msgs(*(None if msgs.get(k) is None else msgs[k].data_ptr() for k in
+                ("arena", "ts", "key_off", "key_len", "val_off", "val_len", "hdr_off", "hdr_len",
+                 "hdr_cnt")))
+    db = torch.frombuffer(bytearray(np.ascontiguousarray(batches, V2_BATCH_DTYPE).tobytes()),
+                          dtype=torch.uint8).to(dev)
+    nmsg = int(msgs["ts"].numel())
+    rec_offs = torch.empty(max(nmsg, 1), dtype=torch.int32, device=dev)
+    sizes = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    s = _stream(stream)
+    _check(lib().rdk_hip_msgset_v2_sizes(C.byref(m), _ptr(db), n, _ptr(rec_offs), _ptr(sizes), s),
+           "msgset_v2_sizes")
+    sz64 = sizes[:n].to(torch.int64)
+    offs = torch.cumsum(sz64, 0) - sz64
+    total = int(sz64.sum()) if n else 0
+    out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    crcs = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if crc else None
+    _check(lib().rdk_hip_msgset_v2_write(C.byref(m), _ptr(db), n, _ptr(rec_offs), _ptr(sizes),
+                                         _ptr(offs), _ptr(out), _ptr(crcs), s), "msgset_v2_write")
+    return out, offs, sizes[:n], (crcs[:n] if crc else None)

@@ -1,0 +1,259 @@
+// records.hip -- MsgVersion 2 record serialisation on gfx950.
+//
+// Replaces, for device-resident messages:
+//   rd_kafka_msgset_writer_write_MessageSet_v2_header  rdkafka_msgset_writer.c:352-403
+//   rd_kafka_msgset_writer_write_msg_v2                 rdkafka_msgset_writer.c:652-754
+//   rd_kafka_msgset_writer_finalize_MessageSet_v2_header rdkafka_msgset_writer.c:1251-1295
+//   (+ calc_crc_v2 :1229-1246 through rdk_hip_msgset_v2_crc FINALIZE)
+// with the batch loop semantics of write_msgq (:804-902): OffsetDelta = index in
+// the batch, TimestampDelta against the first message, MaxTimestamp from 0.
+//
+// Two passes, one workgroup per batch:
+//   sizes: every thread sizes one record (zig-zag varints, rdvarint.h:48-75) and a
+//          workgroup scan places it -> record offsets + batch size;
+//   write: one wavefront per record; lanes write the varint prefix bytes and copy
+//          key / value / header bytes 64 at a time; thread 0 writes the header.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+namespace rdk {
+
+struct Msgs {  // rdk_hip_msgs_t, by value
+  const uint8_t *arena;
+  const int64_t *ts;
+  const uint64_t *key_off;
+  const int32_t *key_len;
+  const uint64_t *val_off;
+  const int32_t *val_len;
+  const uint64_t *hdr_off;
+  const uint32_t *hdr_len;
+  const int32_t *hdr_cnt;
+};
+
+struct Batch {  // rdk_hip_v2_batch_t
+  uint32_t first_msg, msg_count;
+  int64_t producer_id;
+  int32_t base_sequence;
+  int16_t producer_epoch;
+  int16_t attributes;
+};
+
+__device__ __forceinline__ uint64_t zigzag(int64_t v) {
+  return (uint64_t(v) << 1) ^ uint64_t(v >> 63);
+}
+// encoded size of an unsigned LEB128 value (rdvarint.h:48-63): at least one byte
+__device__ __forceinline__ uint32_t vsize(uint64_t u) {
+  const uint32_t bits = u ? 64u - uint32_t(__builtin_clzll(u)) : 1u;
+  return (bits + 6u) / 7u;
+}
+// byte i of an n-byte LEB128 encoding of u
+__device__ __forceinline__ uint32_t vbyte(uint64_t u, uint32_t i, uint32_t n) {
+  return uint32_t((u >> (7u * i)) & 0x7fu) | (i + 1u < n ? 0x80u : 0u);
+}
+
+struct Rec {  // one record's fields (rdkafka_msgset_writer.c:684-716)
+  uint64_t uL, uT, uO, uK, uV, uH;
+  uint32_t sL, sT, sO, sK, sV, sH;
+  uint32_t kb, vb, hb;
+  uint32_t size;  // sL + MessageSize
+};
+
+__device__ __forceinline__ Rec rec_fields(const Msgs &m, uint32_t msg, uint32_t k, int64_t base_ts) {
+  Rec r;
+  const int32_t kl = m.key_len[msg], vl = m.val_len[msg];
+  const int32_t hc = m.hdr_cnt ? m.hdr_cnt[msg] : 0;
+  r.hb = m.hdr_len ? m.hdr_len[msg] : 0u;
+  r.kb = kl > 0 ? uint32_t(kl) : 0u;
+  r.vb = vl > 0 ? uint32_t(vl) : 0u;
+  r.uT = zigzag(m.ts[msg] - base_ts);
+  r.uO = zigzag(int64_t(k));
+  r.uK = zigzag(kl);
+  r.uV = zigzag(vl);
+  r.uH = zigzag(hc);
+  r.sT = vsize(r.uT);
+  r.sO = vsize(r.uO);
+  r.sK = vsize(r.uK);
+  r.sV = vsize(r.uV);
+  r.sH = vsize(r.uH);
+  const uint32_t msz = 1u + r.sT + r.sO + r.sK + r.kb + r.sV + r.vb + r.sH + r.hb;  // :703
+  r.uL = zigzag(int64_t(msz));
+  r.sL = vsize(r.uL);
+  r.size = r.sL + msz;
+  return r;
+}
+
+constexpr int kRecBlock = 256;
+
+// ---- pass 1: record offsets (from the batch start, header included) and batch sizes
+__global__ __launch_bounds__(kRecBlock) void v2_sizes_kernel(Msgs m, const Batch *__restrict__ batches,
+                                                            uint32_t *__restrict__ rec_offs,
+                                                            uint32_t *__restrict__ batch_sizes) {
+  __shared__ uint32_t wsum[kRecBlock / 64];
+  const Batch b = batches[blockIdx.x];
+  const int64_t base_ts = b.msg_count ? m.ts[b.first_msg] : 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t run = 61u;  // RD_KAFKAP_MSGSET_V2_SIZE
+  for (uint32_t c = 0; c < b.msg_count; c += kRecBlock) {
+    const uint32_t k = c + threadIdx.x;
+    const uint32_t sz = k < b.msg_count ? rec_fields(m, b.first_msg + k, k, base_ts).size : 0u;
+    // inclusive wave scan, then across the block's waves
+    uint32_t x = sz;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kRecBlock / 64; ++i) {
+      const uint32_t t = wsum[i];
+      before += i < w ? t : 0u;
+      total += t;
+    }
+    if (k < b.msg_count) rec_offs[b.first_msg + k] = run + before + x - sz;
+    run += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) batch_sizes[blockIdx.x] = run;
+}
+
+__device__ __forceinline__ void st_be(uint8_t *p, uint64_t v, int n) {
+  for (int i = 0; i < n; ++i) p[i] = uint8_t(v >> (8 * (n - 1 - i)));
+}
+
+// ---- pass 2: header + records
+__global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch *__restrict__ batches,
+                                                            const uint32_t *__restrict__ rec_offs,
+                                                            const uint32_t *__restrict__ batch_sizes,
+                                                            const uint64_t *__restrict__ out_offs,
+                                                            uint8_t *__restrict__ out) {
+  __shared__ int64_t wmax[kRecBlock / 64];
+  const Batch b = batches[blockIdx.x];
+  uint8_t *bo = out + out_offs[blockIdx.x];
+  const int64_t base_ts = b.msg_count ? m.ts[b.first_msg] : 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int kWaves = kRecBlock / 64;
+  int64_t mx = 0;  // MaxTimestamp starts at 0 (write_msgq :813, :891)
+  for (uint32_t k = uint32_t(w); k < b.msg_count; k += kWaves) {
+    const uint32_t msg = b.first_msg + k;
+    const Rec r = rec_fields(m, msg, k, base_ts);
+    const int64_t t = m.ts[msg];
+    mx = t > mx ? t : mx;
+    uint8_t *p = bo + rec_offs[msg];
+    // Length, Attributes (0), TimestampDelta, OffsetDelta, KeyLen (:717-731)
+    const uint32_t p1 = r.sL + 1u + r.sT + r.sO + r.sK;
+    const uint32_t j = uint32_t(lane);
+    if (j < p1) {
+      uint32_t v;
+      if (j < r.sL) v = vbyte(r.uL, j, r.sL);
+      else if (j == r.sL) v = 0u;
+      else if (j < r.sL + 1u + r.sT) v = vbyte(r.uT, j - r.sL - 1u, r.sT);
+      else if (j < r.sL + 1u + r.sT + r.sO) v = vbyte(r.uO, j - r.sL - 1u - r.sT, r.sO);
+      else v = vbyte(r.uK, j - r.sL - 1u - r.sT - r.sO, r.sK);
+      p[j] = uint8_t(v);
+    }
+    p += p1;
+    const uint8_t *kp = m.arena + (r.kb ? m.key_off[msg] : 0);
+    for (uint32_t i = j; i < r.kb; i += 64) p[i] = kp[i];  // Key (:734)
+    p += r.kb;
+    if (j < r.sV) p[j] = uint8_t(vbyte(r.uV, j, r.sV));    // ValueLen (:738)
+    p += r.sV;
+    const uint8_t *vp = m.arena + (r.vb ? m.val_off[msg] : 0);
+    for (uint32_t i = j; i < r.vb; i += 64) p[i] = vp[i];  // Value (:741)
+    p += r.vb;
+    if (j < r.sH) p[j] = uint8_t(vbyte(r.uH, j, r.sH));    // HeaderCount (:745)
+    p += r.sH;
+    const uint8_t *hp = m.arena + (r.hb ? m.hdr_off[msg] : 0);
+    for (uint32_t i = j; i < r.hb; i += 64) p[i] = hp[i];  // Headers (:748)
+  }
+  // MaxTimestamp: block max
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const int64_t y = __shfl_xor(mx, d);
+    mx = y > mx ? y : mx;
+  }
+  if (lane == 0) wmax[w] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t M = 0;
+    for (int i = 0; i < kWaves; ++i) M = wmax[i] > M ? wmax[i] : M;
+    const uint32_t size = batch_sizes[blockIdx.x];
+    st_be(bo + 0, 0, 8);                                   // BaseOffset (:362)
+    st_be(bo + 8, size - 12u, 4);                          // Length (:1265)
+    st_be(bo + 12, 0, 4);                                  // PartitionLeaderEpoch (:368)
+    bo[16] = 2;                                            // Magic (:371)
+    st_be(bo + 17, 0, 4);                                  // CRC: calc_crc_v2 later
+    st_be(bo + 21, uint16_t(b.attributes), 2);             // Attributes (:1271)
+    st_be(bo + 23, uint32_t(b.msg_count - 1u), 4);         // LastOffsetDelta (:1275)
+    st_be(bo + 27, uint64_t(base_ts), 8);                  // BaseTimestamp (:1279)
+    st_be(bo + 35, uint64_t(M), 8);                        // MaxTimestamp (:1283)
+    st_be(bo + 43, uint64_t(b.producer_id), 8);            // ProducerId (:392)
+    st_be(bo + 51, uint16_t(b.producer_epoch), 2);         // ProducerEpoch (:395)
+    st_be(bo + 53, uint32_t(b.base_sequence), 4);          // BaseSequence (:1287)
+    st_be(bo + 57, b.msg_count, 4);                        // RecordCount (:1291)
+  }
+}
+
+}  // namespace rdk
+
+using namespace rdk;
+
+static_assert(sizeof(rdk_hip_msgs_t) == sizeof(Msgs), "rdk_hip_msgs_t layout");
+static_assert(sizeof(rdk_hip_v2_batch_t) == sizeof(Batch), "rdk_hip_v2_batch_t layout");
+
+static bool msgs_ok(const rdk_hip_msgs_t *m) {
+  return m && m->arena && m->timestamp && m->key_off && m->key_len && m->value_off &&
+         m->value_len && (!m->header_count || (m->headers_off && m->headers_len));
+}
+
+static Msgs to_msgs(const rdk_hip_msgs_t *m) {
+  Msgs r;
+  r.arena = m->arena;
+  r.ts = m->timestamp;
+  r.key_off = m->key_off;
+  r.key_len = m->key_len;
+  r.val_off = m->value_off;
+  r.val_len = m->value_len;
+  r.hdr_off = m->header_count ? m->headers_off : nullptr;
+  r.hdr_len = m->header_count ? m->headers_len : nullptr;
+  r.hdr_cnt = m->header_count;
+  return r;
+}
+
+RDK_API int rdk_hip_msgset_v2_sizes(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *d_batches,
+                                    uint32_t n, uint32_t *d_rec_offs, uint32_t *d_batch_sizes,
+                                    void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!msgs_ok(msgs) || !d_batches || !d_rec_offs || !d_batch_sizes)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  hipLaunchKernelGGL(v2_sizes_kernel, dim3(n), dim3(kRecBlock), 0, static_cast<hipStream_t>(stream),
+                     to_msgs(msgs), reinterpret_cast<const Batch *>(d_batches), d_rec_offs,
+                     d_batch_sizes);
+  RDK_HIP_CHECK(hipGetLastError());
+  return RDK_HIP_OK;
+}
+
+RDK_API int rdk_hip_msgset_v2_write(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *d_batches,
+                                    uint32_t n, const uint32_t *d_rec_offs,
+                                    const uint32_t *d_batch_sizes, const uint64_t *d_out_offs,
+                                    uint8_t *d_out, uint32_t *d_crc, void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!msgs_ok(msgs) || !d_batches || !d_rec_offs || !d_batch_sizes || !d_out_offs || !d_out)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(v2_write_kernel, dim3(n), dim3(kRecBlock), 0, s, to_msgs(msgs),
+                     reinterpret_cast<const Batch *>(d_batches), d_rec_offs, d_batch_sizes,
+                     d_out_offs, d_out);
+  RDK_HIP_CHECK(hipGetLastError());
+  if (d_crc)  // calc_crc_v2 (:1229-1246): the batch size is its capacity
+    return rdk_hip_msgset_v2_crc(d_out, d_out_offs, d_batch_sizes, d_crc, n,
+                                 RDK_HIP_V2_CRC_FINALIZE, stream);
+  return RDK_HIP_OK;
+}

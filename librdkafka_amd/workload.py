@@ -68,3 +68,58 @@ def json_v2_batch(payload: bytes, base_offset: int = 0) -> bytearray:
     hdr = bytearray(v2_header(0, V2_HEADER + len(payload) + ((8 - (V2_HEADER + len(payload)) % 8) % 8)))
     struct.pack_into(">i", hdr, V2_OF_LENGTH, V2_HEADER + len(payload) - 12)
     return hdr + payload
+
+
+def gen_messages(n: int, seed: int = 42, headers: bool = True) -> dict:
+    """Synthetic producer messages for the MsgVersion 2 record writer (numpy SoA).
+
+    Values are JSON-like records (`gen_json` lines, ~95 B); keys are "k<id>"
+    (every 7th null, every 11th empty); every 13th value is null; timestamps
+    advance 0-3 ms with every 17th message stepping back (negative deltas);
+    every 5th message carries 1-2 headers, serialised as on the wire
+    (varint name length, name, varint value length, value;
+    rdkafka_msgset_writer.c:558-568).
+    """
+    def zz(v):
+        u = (v << 1) ^ (v >> 63)
+        u &= (1 << 64) - 1
+        out = bytearray()
+        while True:
+            out.append((u & 0x7F) | (0x80 if u > 0x7F else 0))
+            u >>= 7
+            if not u:
+                return bytes(out)
+    lines = gen_json(n * 100 + 4096, seed).split(b"\n")
+    arena = bytearray()
+    ts = np.zeros(n, np.int64)
+    key_off = np.zeros(n, np.uint64); key_len = np.zeros(n, np.int32)
+    val_off = np.zeros(n, np.uint64); val_len = np.zeros(n, np.int32)
+    hdr_off = np.zeros(n, np.uint64); hdr_len = np.zeros(n, np.uint32)
+    hdr_cnt = np.zeros(n, np.int32)
+    t = 1600000000000
+    s = seed & 0xFFFFFFFF
+    for i in range(n):
+        s = (s * 1103515245 + 12345) & 0xFFFFFFFF
+        t += (s >> 8) % 4 if i % 17 else -((s >> 8) % 50)
+        ts[i] = t
+        if i % 7 == 0:
+            key_len[i] = -1
+        else:
+            k = b"" if i % 11 == 0 else b"k%d" % i
+            key_off[i] = len(arena); key_len[i] = len(k); arena += k
+        if i % 13 == 0:
+            val_len[i] = -1
+        else:
+            v = lines[i % len(lines)]
+            val_off[i] = len(arena); val_len[i] = len(v); arena += v
+        if headers and i % 5 == 0:
+            h = bytearray()
+            for j in range(1 + (i // 5) % 2):
+                name, val = b"h%d" % j, (b"v%d" % i if j == 0 else None)
+                h += zz(len(name)) + name
+                h += zz(len(val)) + val if val is not None else zz(-1)
+            hdr_off[i] = len(arena); hdr_len[i] = len(h); hdr_cnt[i] = 1 + (i // 5) % 2
+            arena += h
+    return {"arena": np.frombuffer(bytes(arena) or b"\0", np.uint8).copy(), "ts": ts,
+            "key_off": key_off, "key_len": key_len, "val_off": val_off, "val_len": val_len,
+            "hdr_off": hdr_off, "hdr_len": hdr_len, "hdr_cnt": hdr_cnt}

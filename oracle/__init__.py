@@ -77,6 +77,16 @@ def lib():
         L.or_lz4f_decompress_batches_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                                     C.c_int]
+        vp = C.c_void_p
+        L.or_varint_enc_i64.restype = C.c_size_t
+        L.or_varint_enc_i64.argtypes = [vp, C.c_int64]
+        L.or_varint_dec_i64.restype = C.c_size_t
+        L.or_varint_dec_i64.argtypes = [vp, C.c_size_t, C.POINTER(C.c_int64)]
+        L.or_msgset_v2_write.restype = C.c_size_t
+        L.or_msgset_v2_write.argtypes = [vp] * 9 + [C.c_uint32, C.c_uint32, C.c_int64, C.c_int16,
+                                                    C.c_int32, C.c_int16, vp]
+        L.or_msgset_v2_index.restype = C.c_long
+        L.or_msgset_v2_index.argtypes = [vp, C.c_size_t, C.c_int64, C.c_int64] + [vp] * 8 + [C.c_long]
         _lib = L
     return _lib
 
@@ -256,3 +266,59 @@ def ref_lz4f_compress_prefs(data: bytes, linked=0, block_size_id=4, block_checks
     res = C.string_at(out, n.value)
     R.ref_free(out)
     return res
+
+
+# ---- MsgVersion 2 records (msgset_oracle.c) ---------------------------------
+def varint_enc(num: int) -> bytes:
+    """rdvarint.h:67 rd_uvarint_enc_i64 (zig-zag + LEB128)."""
+    b = C.create_string_buffer(16)
+    n = lib().or_varint_enc_i64(b, num)
+    return b.raw[:n]
+
+
+def varint_dec(data: bytes) -> tuple[int, int]:
+    """rdvarint.h:132 rd_varint_dec_i64 -> (value, bytes read); bytes read 0 = failure."""
+    v = C.c_int64()
+    n = lib().or_varint_dec_i64(_buf(data), len(data), C.byref(v))
+    return v.value, n
+
+
+def _np_ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def msgset_v2_write(msgs: dict, first: int, cnt: int, producer_id: int = -1,
+                    producer_epoch: int = -1, base_sequence: int = -1, attributes: int = 0) -> bytes:
+    """One uncompressed MsgVersion 2 batch of messages [first, first+cnt), as
+    rdkafka_msgset_writer.c writes it.  `msgs`: numpy arrays arena (u8), ts (i64),
+    key_off (u64), key_len (i32, -1 null), val_off, val_len, and optionally
+    hdr_off (u64), hdr_len (u32), hdr_cnt (i32)."""
+    import numpy as np
+    kl, vl = msgs["key_len"], msgs["val_len"]
+    hl = msgs.get("hdr_len")
+    cap = 61 + int(cnt) * 40 + int(np.maximum(kl[first:first + cnt], 0).sum()) + \
+        int(np.maximum(vl[first:first + cnt], 0).sum()) + \
+        (int(hl[first:first + cnt].sum()) if hl is not None else 0)
+    out = np.zeros(cap, dtype=np.uint8)
+    n = lib().or_msgset_v2_write(
+        _np_ptr(msgs["arena"]), _np_ptr(msgs["ts"]), _np_ptr(msgs["key_off"]), _np_ptr(kl),
+        _np_ptr(msgs["val_off"]), _np_ptr(vl), _np_ptr(msgs.get("hdr_off")), _np_ptr(hl),
+        _np_ptr(msgs.get("hdr_cnt")), first, cnt, producer_id, producer_epoch, base_sequence,
+        attributes, _np_ptr(out))
+    return bytes(out[:n])
+
+
+def msgset_v2_index(records: bytes, base_offset: int = 0, base_ts: int = 0, max_rows=None):
+    """rdkafka_msgset_reader.c:715-927 over a batch's records -> (n, rows dict);
+    n < 0: record -n-1 failed to parse."""
+    import numpy as np
+    m = max_rows if max_rows is not None else max(1, len(records) // 7 + 1)
+    rows = {k: np.zeros(m, dtype=t) for k, t in (("offset", np.int64), ("timestamp", np.int64),
+                                                  ("key_off", np.uint32), ("key_len", np.int32),
+                                                  ("val_off", np.uint32), ("val_len", np.int32),
+                                                  ("hdr_off", np.uint32), ("hdr_len", np.uint32))}
+    rec = np.frombuffer(records, dtype=np.uint8) if records else np.zeros(1, dtype=np.uint8)
+    n = lib().or_msgset_v2_index(
+        _np_ptr(rec), len(records), base_offset, base_ts, *(_np_ptr(rows[k]) for k in
+        ("offset", "timestamp", "key_off", "key_len", "val_off", "val_len", "hdr_off", "hdr_len")), m)
+    return n, {k: v[:max(n, 0)] for k, v in rows.items()}

@@ -96,6 +96,25 @@ int or_lz4f_decompress_batches_mt(const uint8_t *base, const uint64_t *offs,
                                   const uint32_t *out_caps, uint32_t *out_lens,
                                   int threads);
 
+
+/* ---- MsgVersion 2 records (msgset_oracle.c) ---------- */
+/* rdvarint.h:48-75 / :114-141 (zig-zag varints) */
+size_t   or_varint_enc_i64(uint8_t *dst, int64_t num);
+size_t   or_varint_dec_i64(const uint8_t *src, size_t srcsize, int64_t *nump);
+/* rdkafka_msgset_writer.c:352-403 + :652-754 + :1251-1295: one uncompressed batch */
+size_t   or_msgset_v2_write(const uint8_t *arena, const int64_t *ts, const uint64_t *key_off,
+                            const int32_t *key_len, const uint64_t *val_off,
+                            const int32_t *val_len, const uint64_t *hdr_off,
+                            const uint32_t *hdr_len, const int32_t *hdr_cnt, uint32_t first,
+                            uint32_t cnt, int64_t producer_id, int16_t producer_epoch,
+                            int32_t base_sequence, int16_t attributes, uint8_t *out);
+/* rdkafka_msgset_reader.c:715-927: index rows of a batch's records */
+long     or_msgset_v2_index(const uint8_t *rec, size_t len, int64_t base_offset,
+                            int64_t base_ts, int64_t *offset, int64_t *timestamp,
+                            uint32_t *key_off, int32_t *key_len, uint32_t *val_off,
+                            int32_t *val_len, uint32_t *hdr_off, uint32_t *hdr_len,
+                            long max_rows);
+
 #ifdef __cplusplus
 }
 #endif

@@ -225,6 +225,93 @@ def bench_consumer(args, rank, world, n=None):
             "alg_bytes": csum + (csum + 61 * n) + n * JSON_BATCH}
 
 
+def tiled_messages(n_batches, per_batch, seed=42):
+    """n_batches x per_batch producer messages (~100 B JSON values, keys, nulls,
+    headers: workload.gen_messages) for the record writer: 16384 distinct messages
+    tiled, sharing one arena; timestamps continue across tiles."""
+    import numpy as np
+    import torch
+    from librdkafka_amd import workload as W
+    base = W.gen_messages(16384, seed=seed)
+    n = n_batches * per_batch
+    reps = (n + 16383) // 16384
+    d = {}
+    for k, v in base.items():
+        if k == "arena":
+            d[k] = torch.from_numpy(v).cuda()
+            continue
+        t = np.tile(v, reps)[:n]
+        if k == "ts":
+            span = int(v.max() - v.min()) + 1
+            t = t + np.repeat(np.arange(reps, dtype=np.int64) * span, 16384)[:n]
+        if t.dtype == np.uint64:
+            t = t.view(np.int64)
+        elif t.dtype == np.uint32:
+            t = t.view(np.int32)
+        d[k] = torch.from_numpy(np.ascontiguousarray(t)).cuda()
+    payload = int(np.maximum(base["key_len"], 0).sum() + np.maximum(base["val_len"], 0).sum()
+                  + base["hdr_len"].sum()) * n // 16384
+    return base, d, payload
+
+
+def bench_serialize(args, rank, world, n=None, per_batch=9500):
+    """SURVEY §8f rank 1 / configs[4] shape: linger-accumulated ~1 MiB MsgVersion 2
+    batches of ~100-byte JSON records built on the device (record sizes + scan, record
+    writer, CRC32C finalize) from per-message key / value / header arrays."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import librdkafka_amd as L
+    n = n or args.partitions // world
+    base, d, payload = tiled_messages(n, per_batch, seed=42 + rank)
+    b = np.zeros(n, dtype=L.V2_BATCH_DTYPE)
+    b["first_msg"] = np.arange(n) * per_batch
+    b["msg_count"] = per_batch
+    b["producer_id"] = -1
+    b["base_sequence"] = -1
+    b["producer_epoch"] = -1
+    out, offs, sizes, crcs = L.msgset_v2_build(d, b, crc=True)
+    m = L._Msgs(*(d[k].data_ptr() for k in ("arena", "ts", "key_off", "key_len", "val_off",
+                                            "val_len", "hdr_off", "hdr_len", "hdr_cnt")))
+    rec_offs = torch.empty(n * per_batch, dtype=torch.int32, device="cuda")
+    max_ts = torch.empty(n, dtype=torch.int64, device="cuda")
+    s = L._stream(None)
+    lib = L.lib()
+
+    def step():
+        lib.rdk_hip_msgset_v2_sizes(C.byref(m), b.ctypes.data, n, L._ptr(rec_offs), L._ptr(sizes),
+                                    L._ptr(max_ts), s)
+        lib.rdk_hip_msgset_v2_write(C.byref(m), b.ctypes.data, n, L._ptr(rec_offs), L._ptr(sizes),
+                                    L._ptr(max_ts), L._ptr(offs), L._ptr(out), L._ptr(crcs), s)
+
+    ms, kms = _timed(step, args.steps, args.warmup, world)
+    total = int(sizes.to(torch.int64).sum())
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    L.msgset_v2_crc(out, offs, sizes, st, L.V2_CRC_VERIFY)
+    assert int(st.abs().sum()) == 0
+    # per message: 48 B of metadata read, its payload bytes read; every batch byte written
+    return {"ms": ms, "kernel_ms": kms, "bytes": total, "records": n,
+            "alg_bytes": payload + 48 * n * per_batch + total,
+            "host_sample": (base, per_batch)}
+
+
+def cpu_baseline_serialize(base, per_batch, seconds=3.0):
+    """The oracle restatement of rd_kafka_msgset_writer_write_msg_v2 + header finalize +
+    calc_crc_v2 (msgset_oracle.c), one host thread, batches of the same messages."""
+    import oracle
+    per_batch = min(per_batch, 16384)
+    passes, nbytes, t0 = 0, 0, time.perf_counter()
+    while True:
+        nbytes += len(oracle.msgset_v2_write(base, 0, per_batch))
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(nbytes / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{passes} batches x {per_batch} JSON messages, write_msg_v2 + finalize + "
+                      f"CRC32C restated, {cpu_model()}"}
+
+
 def bench_producer(args, rank, world, n=None, threads=None, mode=1, slot_mib=None):
     """configs[4] (full producer pipeline), bounded: n toppars per GPU each
     hand one linger-accumulated 1 MiB batch of JSON records (61-byte v2
@@ -396,6 +483,13 @@ def leg_line(name, res, steps, world, cpu=None):
     return d
 
 
+def serialize_leg(rank, world, no_cpu):
+    res = bench_serialize(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
+    cpu = None if no_cpu else cpu_baseline_serialize(*res.pop("host_sample"))
+    res.pop("host_sample", None)
+    return leg_line("serialize", res, 3, world, cpu)
+
+
 # HBM bytes per launch from rocprofv3 PMC passes on this kernel and workload
 # (scripts/profile_crc.sh -> scripts/pmc_summary.py; FETCH_SIZE x2 on gfx950).
 # Counters cannot be read in-process, so the committed summary of the same
@@ -423,7 +517,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="crc", choices=["crc", "lz4c", "lz4c_fast", "consumer", "producer"])
+    ap.add_argument("--workload", default="crc",
+                    choices=["crc", "lz4c", "lz4c_fast", "consumer", "producer", "serialize"])
     ap.add_argument("--batches", type=int, default=CRC_BATCHES)
     ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -446,14 +541,20 @@ def main():
             res = bench_lz4c(args, rank, world, fast=args.workload == "lz4c_fast")
         elif args.workload == "producer":
             res = bench_producer(args, rank, world)
+        elif args.workload == "serialize":
+            res = bench_serialize(args, rank, world)
         else:
             res = bench_consumer(args, rank, world)
         t_max = max_over_ranks(res["ms"], world)
         if rank == 0:
             cpu = None
             if not args.no_cpu_baseline and world == 1:
-                cpu = cpu_baseline_lz4("decompress" if args.workload == "consumer"
-                                       else "compress")
+                if args.workload == "serialize":
+                    cpu = cpu_baseline_serialize(*res["host_sample"])
+                else:
+                    cpu = cpu_baseline_lz4("decompress" if args.workload == "consumer"
+                                           else "compress")
+            res.pop("host_sample", None)
             res["ms"] = t_max
             print(json.dumps({"workload": args.workload, "n_gpus": world, "steps": args.steps,
                               **leg_line(args.workload, res, args.steps, world, cpu)}), flush=True)
@@ -515,6 +616,7 @@ def main():
                 "consumer_crc_verify_lz4f_decompress_1MiB": leg_line(
                     "consumer", bench_consumer(argparse.Namespace(steps=3, warmup=1, partitions=1024),
                                                rank, world), 3, 1, cpu("decompress")),
+                "v2_record_serialize_1MiB_json": serialize_leg(rank, world, args.no_cpu_baseline),
                 "producer_pipeline_1MiB_json_pcie": leg_line(
                     "producer", bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512),
                                                rank, world), 2, 1, cpu("compress")),

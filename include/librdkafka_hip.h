@@ -212,17 +212,19 @@ typedef struct rdk_hip_v2_batch_s { /* one MessageSet: messages [first_msg, +msg
   int16_t producer_epoch;           /* (:395) */
   int16_t attributes;               /* codec bits etc. (:1271) */
 } rdk_hip_v2_batch_t;
-/* Pass 1: d_rec_offs[m] = offset of message m's record from its batch start
- * (header included), d_batch_sizes[b] = 61 + records bytes. */
-int rdk_hip_msgset_v2_sizes(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *d_batches,
+/* `batches` are HOST descriptors (copied to the device on `stream`).
+ * Pass 1: d_rec_offs[m] = offset of message m's record from its batch start (header
+ * included), d_batch_sizes[b] = 61 + records bytes, d_max_ts[b] = MaxTimestamp. */
+int rdk_hip_msgset_v2_sizes(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *batches,
                             uint32_t n_batches, uint32_t *d_rec_offs, uint32_t *d_batch_sizes,
-                            void *stream);
+                            int64_t *d_max_ts, void *stream);
 /* Pass 2: batch b written at d_out + d_out_offs[b] (d_batch_sizes[b] bytes); with d_crc
  * the CRC32C is stored at offset 17 as calc_crc_v2 does (:1229-1246) and in d_crc[b]. */
-int rdk_hip_msgset_v2_write(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *d_batches,
+int rdk_hip_msgset_v2_write(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *batches,
                             uint32_t n_batches, const uint32_t *d_rec_offs,
-                            const uint32_t *d_batch_sizes, const uint64_t *d_out_offs,
-                            uint8_t *d_out, uint32_t *d_crc, void *stream);
+                            const uint32_t *d_batch_sizes, const int64_t *d_max_ts,
+                            const uint64_t *d_out_offs, uint8_t *d_out, uint32_t *d_crc,
+                            void *stream);
 
 /* Deterministic synthetic workloads generated on the device (bench/tests).
  * v2 batches: n batches of `batch_size` bytes at i*batch_size: a valid 61-byte

@@ -116,9 +116,9 @@ def lib():
     L.rdk_hip_gen_json.restype = None
     L.rdk_hip_gen_json.argtypes = [vp, sz, u32]
     L.rdk_hip_msgset_v2_sizes.restype = i32
-    L.rdk_hip_msgset_v2_sizes.argtypes = [C.POINTER(_Msgs), vp, u32, vp, vp, vp]
+    L.rdk_hip_msgset_v2_sizes.argtypes = [C.POINTER(_Msgs), vp, u32, vp, vp, vp, vp]
     L.rdk_hip_msgset_v2_write.restype = i32
-    L.rdk_hip_msgset_v2_write.argtypes = [C.POINTER(_Msgs), vp, u32, vp, vp, vp, vp, vp, vp]
+    L.rdk_hip_msgset_v2_write.argtypes = [C.POINTER(_Msgs), vp, u32, vp, vp, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -400,19 +400,20 @@ def msgset_v2_build(msgs: dict, batches: np.ndarray, crc: bool = True, stream=No
     m = _Msgs(*(None if msgs.get(k) is None else msgs[k].data_ptr() for k in
                 ("arena", "ts", "key_off", "key_len", "val_off", "val_len", "hdr_off", "hdr_len",
                  "hdr_cnt")))
-    db = torch.frombuffer(bytearray(np.ascontiguousarray(batches, V2_BATCH_DTYPE).tobytes()),
-                          dtype=torch.uint8).to(dev)
+    hb = np.ascontiguousarray(batches, V2_BATCH_DTYPE)
     nmsg = int(msgs["ts"].numel())
     rec_offs = torch.empty(max(nmsg, 1), dtype=torch.int32, device=dev)
     sizes = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    max_ts = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     s = _stream(stream)
-    _check(lib().rdk_hip_msgset_v2_sizes(C.byref(m), _ptr(db), n, _ptr(rec_offs), _ptr(sizes), s),
-           "msgset_v2_sizes")
+    _check(lib().rdk_hip_msgset_v2_sizes(C.byref(m), hb.ctypes.data, n, _ptr(rec_offs), _ptr(sizes),
+                                         _ptr(max_ts), s), "msgset_v2_sizes")
     sz64 = sizes[:n].to(torch.int64)
     offs = torch.cumsum(sz64, 0) - sz64
     total = int(sz64.sum()) if n else 0
     out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
     crcs = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if crc else None
-    _check(lib().rdk_hip_msgset_v2_write(C.byref(m), _ptr(db), n, _ptr(rec_offs), _ptr(sizes),
-                                         _ptr(offs), _ptr(out), _ptr(crcs), s), "msgset_v2_write")
+    _check(lib().rdk_hip_msgset_v2_write(C.byref(m), hb.ctypes.data, n, _ptr(rec_offs),
+                                         _ptr(sizes), _ptr(max_ts), _ptr(offs), _ptr(out),
+                                         _ptr(crcs), s), "msgset_v2_write")
     return out, offs, sizes[:n], (crcs[:n] if crc else None)

@@ -26,6 +26,7 @@
 #include "common.h"
 #include "crc32c_tables.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -731,6 +732,93 @@ __global__ __launch_bounds__(kV4Block, 1) void crc32c_msgset_v2_v4_kernel(
   }
 }
 
+// ---- few large batches: split each CRC range into nch chunks (more work items than
+// the CUs have group slots), raw CRCs per chunk, then one combine per batch with the
+// GF(2) shift of crc32c.c:144-231 (multiply by x^(8*len) mod P)
+__device__ __forceinline__ void v2_range(const uint8_t *hdr, uint32_t length, uint32_t cap,
+                                         bool &bad, uintptr_t &s, uintptr_t &e) {
+  bad = length < 9u || uint64_t(length) + 12u > cap;  // crc_len = Length-4-1-4
+  s = reinterpret_cast<uintptr_t>(hdr) + 21u;
+  e = reinterpret_cast<uintptr_t>(hdr) + 12u + length;
+}
+__device__ __forceinline__ uint32_t split_chunk(uint32_t len, uint32_t nch) {
+  return (((len + nch - 1u) / nch) + 15u) & ~15u;
+}
+
+__global__ __launch_bounds__(kV4Block, 1) void crc32c_msgset_v2_split_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint32_t *__restrict__ caps, uint32_t n, uint32_t nch, uint32_t *__restrict__ raw,
+    const uint32_t *__restrict__ gtab) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[kCrcV4Words];  // the kernel's only LDS: at 0
+  load_tables_v4(L, gtab);
+  const int lane = threadIdx.x & 63;
+  const uint32_t items = n * nch;
+  const uint32_t stride = gridDim.x * kV4Groups;
+  uint32_t w = blockIdx.x * kV4Groups + (threadIdx.x / kV4Lanes);
+  for (uint32_t w0 = blockIdx.x * kV4Groups; w0 < items; w0 += stride, w += stride) {
+    const bool act = w < items;
+    const uint32_t i = act ? w / nch : 0u, j = act ? w % nch : 0u;
+    const uint8_t *hdr = base + offs[i];
+    bool bad;
+    uintptr_t s, e;
+    v2_range(hdr, be32_at(hdr + 8), caps[i], bad, s, e);
+    const uint32_t C = bad ? 0u : split_chunk(uint32_t(e - s), nch);
+    const uintptr_t cs = s + uintptr_t(j) * C;
+    const uintptr_t ce = cs + C < e ? cs + C : e;
+    const bool on = act && !bad && (j == 0 || cs < e);  // an empty range keeps ~init
+    // chunk 0 carries crc32c()'s initial register; the others are raw (zero) registers
+    const uint32_t r = group_crc_v4(cs, on ? ce : cs, j == 0 ? ~0u : 0u, on, lane,
+                                    (const lds_u32 *)L);
+    if (act && (lane & (kV4Lanes - 1)) == 0) raw[w] = r;
+  }
+}
+
+__device__ uint32_t xpow8n(uint64_t nbytes, const uint32_t *x2n) {  // x^(8*nbytes) mod P
+  uint32_t p = 1u << 31;
+  int k = 3;
+  for (uint64_t n = nbytes; n; n >>= 1, ++k)
+    if (n & 1u) p = multmodp(x2n[k], p);
+  return p;
+}
+
+template <int MODE>
+__global__ void crc32c_msgset_v2_combine_kernel(uint8_t *__restrict__ base,
+                                                const uint64_t *__restrict__ offs,
+                                                const uint32_t *__restrict__ caps, uint32_t n,
+                                                uint32_t nch, const uint32_t *__restrict__ raw,
+                                                uint32_t *__restrict__ out,
+                                                const uint32_t *__restrict__ x2n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t *hdr = base + offs[i];
+  bool bad;
+  uintptr_t s, e;
+  v2_range(hdr, be32_at(hdr + 8), caps[i], bad, s, e);
+  if (bad) {
+    out[i] = (MODE == RDK_HIP_V2_CRC_VERIFY) ? 2u : 0u;
+    return;
+  }
+  const uint32_t len = uint32_t(e - s), C = split_chunk(len, nch);
+  const uint32_t pc = xpow8n(C, x2n);
+  uint32_t r = raw[size_t(i) * nch];
+  for (uint32_t j = 1; j < nch && uint64_t(j) * C < len; ++j) {
+    const uint32_t cl = (uint64_t(j + 1) * C <= len) ? C : len - j * C;
+    r = multmodp(cl == C ? pc : xpow8n(cl, x2n), r) ^ raw[size_t(i) * nch + j];
+  }
+  const uint32_t crc = ~r;
+  if (MODE == RDK_HIP_V2_CRC_VERIFY) {
+    out[i] = (be32_at(hdr + 17) == crc) ? 0u : 1u;
+  } else {
+    out[i] = crc;
+    if (MODE == RDK_HIP_V2_CRC_FINALIZE) {  // rd_kafka_buf_update_i32 (BE)
+      hdr[17] = uint8_t(crc >> 24);
+      hdr[18] = uint8_t(crc >> 16);
+      hdr[19] = uint8_t(crc >> 8);
+      hdr[20] = uint8_t(crc);
+    }
+  }
+}
+
 }  // namespace rdk
 
 // ============================================================ host launchers
@@ -815,7 +903,22 @@ static void launch_v2(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *
 template <int MODE>
 static void launch_v2_any(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *caps,
                           uint32_t *out, uint32_t n, hipStream_t s) {
-  if (crc_variant() == 4)
+  // fewer than 2 batches per group slot of the chip: split every range into chunks
+  constexpr uint32_t kSlots = 256u * kV4Groups;
+  if (crc_variant() == 4 && n <= kSlots / 2) {
+    const uint32_t nch = std::min(64u, kSlots / n);
+    uint32_t *raw = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void **>(&raw), size_t(n) * nch * 4, s) != hipSuccess) {
+      set_error(RDK_HIP_E_NOMEM, "split scratch");
+      return;
+    }
+    const uint32_t items = n * nch;
+    hipLaunchKernelGGL(crc32c_msgset_v2_split_kernel, dim3(crc_grid_v4(items)), dim3(kV4Block),
+                       0, s, b, offs, caps, n, nch, raw, crc_tables_v4_dev(c->device));
+    hipLaunchKernelGGL(crc32c_msgset_v2_combine_kernel<MODE>, dim3((n + 63) / 64), dim3(64), 0,
+                       s, b, offs, caps, n, nch, raw, out, crc_x2n_dev(c->device));
+    (void)hipFreeAsync(raw, s);
+  } else if (crc_variant() == 4)
     hipLaunchKernelGGL(crc32c_msgset_v2_v4_kernel<MODE>, dim3(crc_grid_v4(n)), dim3(kV4Block), 0,
                        s, b, offs, caps, out, n, crc_tables_v4_dev(c->device));
   else if (crc_variant() == 3) launch_v2<3, MODE>(c, b, offs, caps, out, n, s);

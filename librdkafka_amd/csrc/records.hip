@@ -8,11 +8,12 @@
 // with the batch loop semantics of write_msgq (:804-902): OffsetDelta = index in
 // the batch, TimestampDelta against the first message, MaxTimestamp from 0.
 //
-// Two passes, one workgroup per batch:
-//   sizes: every thread sizes one record (zig-zag varints, rdvarint.h:48-75) and a
-//          workgroup scan places it -> record offsets + batch size;
-//   write: one wavefront per record; lanes write the varint prefix bytes and copy
-//          key / value / header bytes 64 at a time; thread 0 writes the header.
+// Workgroups of 256 threads work on chunks of 256 records (grid = chunks x batches):
+//   sizes: a thread sizes one record (zig-zag varints, rdvarint.h:48-75), a chunk scan
+//          plus a per-batch scan of chunk totals place it -> record offsets, batch size;
+//   write: one lane per record (256 records of a batch in flight per workgroup): the
+//          varint prefix bytes, then key / value / header bytes 16 loads ahead of their
+//          stores; thread 0 writes the header.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -83,118 +84,169 @@ __device__ __forceinline__ Rec rec_fields(const Msgs &m, uint32_t msg, uint32_t 
   return r;
 }
 
-constexpr int kRecBlock = 256;
+constexpr int kRecBlock = 256;  // records per chunk = threads per workgroup
 
-// ---- pass 1: record offsets (from the batch start, header included) and batch sizes
-__global__ __launch_bounds__(kRecBlock) void v2_sizes_kernel(Msgs m, const Batch *__restrict__ batches,
+// ---- sizes, 1/3: per chunk of 256 records: sizes, chunk-local exclusive offsets,
+// chunk total and chunk MaxTimestamp.  grid (chunks, batches)
+__global__ __launch_bounds__(kRecBlock) void v2_chunk_kernel(Msgs m, const Batch *__restrict__ batches,
+                                                            uint32_t nchunk,
                                                             uint32_t *__restrict__ rec_offs,
-                                                            uint32_t *__restrict__ batch_sizes) {
+                                                            uint32_t *__restrict__ chunk_tot,
+                                                            int64_t *__restrict__ chunk_max) {
   __shared__ uint32_t wsum[kRecBlock / 64];
-  const Batch b = batches[blockIdx.x];
-  const int64_t base_ts = b.msg_count ? m.ts[b.first_msg] : 0;
+  __shared__ int64_t wmax[kRecBlock / 64];
+  const Batch b = batches[blockIdx.y];
+  const uint32_t c = blockIdx.x;
+  if (c * kRecBlock >= b.msg_count) {
+    if (threadIdx.x == 0) {
+      chunk_tot[blockIdx.y * nchunk + c] = 0u;
+      chunk_max[blockIdx.y * nchunk + c] = 0;
+    }
+    return;
+  }
+  const int64_t base_ts = m.ts[b.first_msg];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t k = c * kRecBlock + threadIdx.x;
+  const bool on = k < b.msg_count;
+  const uint32_t sz = on ? rec_fields(m, b.first_msg + k, k, base_ts).size : 0u;
+  int64_t mx = on ? m.ts[b.first_msg + k] : 0;  // MaxTimestamp from 0 (write_msgq :813)
+  uint32_t x = sz;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+    const int64_t z = __shfl_xor(mx, d);
+    mx = z > mx ? z : mx;
+  }
+  if (lane == 63) wsum[w] = x;
+  if (lane == 0) wmax[w] = mx;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  int64_t M = 0;
+#pragma unroll
+  for (int i = 0; i < kRecBlock / 64; ++i) {
+    before += i < w ? wsum[i] : 0u;
+    total += wsum[i];
+    M = wmax[i] > M ? wmax[i] : M;
+  }
+  if (on) rec_offs[b.first_msg + k] = before + x - sz;
+  if (threadIdx.x == 0) {
+    chunk_tot[blockIdx.y * nchunk + c] = total;
+    chunk_max[blockIdx.y * nchunk + c] = M;
+  }
+}
+
+// ---- sizes, 2/3: per batch: scan of its chunk totals (in place -> chunk bases from
+// the batch start, header included), batch size, MaxTimestamp.  grid (batches), 64 threads
+__global__ __launch_bounds__(64) void v2_batch_kernel(uint32_t nchunk, uint32_t *__restrict__ chunk_tot,
+                                                     const int64_t *__restrict__ chunk_max,
+                                                     uint32_t *__restrict__ batch_sizes,
+                                                     int64_t *__restrict__ max_ts) {
+  const int lane = threadIdx.x;
+  uint32_t *t = chunk_tot + blockIdx.x * nchunk;
+  const int64_t *cm = chunk_max + blockIdx.x * nchunk;
   uint32_t run = 61u;  // RD_KAFKAP_MSGSET_V2_SIZE
-  for (uint32_t c = 0; c < b.msg_count; c += kRecBlock) {
-    const uint32_t k = c + threadIdx.x;
-    const uint32_t sz = k < b.msg_count ? rec_fields(m, b.first_msg + k, k, base_ts).size : 0u;
-    // inclusive wave scan, then across the block's waves
-    uint32_t x = sz;
+  int64_t mx = 0;
+  for (uint32_t c0 = 0; c0 < nchunk; c0 += 64) {
+    const uint32_t c = c0 + uint32_t(lane);
+    const uint32_t v = c < nchunk ? t[c] : 0u;
+    int64_t z = c < nchunk ? cm[c] : 0;
+    uint32_t x = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(x, d);
       if (lane >= d) x += y;
+      const int64_t q = __shfl_xor(z, d);
+      z = q > z ? q : z;
     }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (int i = 0; i < kRecBlock / 64; ++i) {
-      const uint32_t t = wsum[i];
-      before += i < w ? t : 0u;
-      total += t;
-    }
-    if (k < b.msg_count) rec_offs[b.first_msg + k] = run + before + x - sz;
-    run += total;
-    __syncthreads();
+    if (c < nchunk) t[c] = run + x - v;
+    run += __shfl(x, 63);
+    mx = z > mx ? z : mx;
   }
-  if (threadIdx.x == 0) batch_sizes[blockIdx.x] = run;
+  if (lane == 0) {
+    batch_sizes[blockIdx.x] = run;
+    max_ts[blockIdx.x] = mx;
+  }
+}
+
+// ---- sizes, 3/3: record offsets from the batch start.  grid (chunks, batches)
+__global__ __launch_bounds__(kRecBlock) void v2_fixup_kernel(const Batch *__restrict__ batches,
+                                                            uint32_t nchunk,
+                                                            const uint32_t *__restrict__ chunk_base,
+                                                            uint32_t *__restrict__ rec_offs) {
+  const Batch b = batches[blockIdx.y];
+  const uint32_t k = blockIdx.x * kRecBlock + threadIdx.x;
+  if (k < b.msg_count) rec_offs[b.first_msg + k] += chunk_base[blockIdx.y * nchunk + blockIdx.x];
 }
 
 __device__ __forceinline__ void st_be(uint8_t *p, uint64_t v, int n) {
   for (int i = 0; i < n; ++i) p[i] = uint8_t(v >> (8 * (n - 1 - i)));
 }
 
-// ---- pass 2: header + records
+// n bytes src -> dst, 16 at a time: all loads of a round first (clamped to the last
+// byte, so always in bounds), then the stores
+__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n) {
+  for (uint32_t i = 0; i < n; i += 16) {
+    uint8_t t[16];
+#pragma unroll
+    for (uint32_t u = 0; u < 16; ++u) t[u] = src[(i + u < n) ? i + u : n - 1u];
+#pragma unroll
+    for (uint32_t u = 0; u < 16; ++u)
+      if (i + u < n) dst[i + u] = t[u];
+  }
+}
+
+// ---- write: one lane per record, grid (chunks, batches); chunk 0 also writes the header
 __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch *__restrict__ batches,
                                                             const uint32_t *__restrict__ rec_offs,
                                                             const uint32_t *__restrict__ batch_sizes,
+                                                            const int64_t *__restrict__ max_ts,
                                                             const uint64_t *__restrict__ out_offs,
                                                             uint8_t *__restrict__ out) {
-  __shared__ int64_t wmax[kRecBlock / 64];
-  const Batch b = batches[blockIdx.x];
-  uint8_t *bo = out + out_offs[blockIdx.x];
-  const int64_t base_ts = b.msg_count ? m.ts[b.first_msg] : 0;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  constexpr int kWaves = kRecBlock / 64;
-  int64_t mx = 0;  // MaxTimestamp starts at 0 (write_msgq :813, :891)
-  for (uint32_t k = uint32_t(w); k < b.msg_count; k += kWaves) {
-    const uint32_t msg = b.first_msg + k;
-    const Rec r = rec_fields(m, msg, k, base_ts);
-    const int64_t t = m.ts[msg];
-    mx = t > mx ? t : mx;
-    uint8_t *p = bo + rec_offs[msg];
-    // Length, Attributes (0), TimestampDelta, OffsetDelta, KeyLen (:717-731)
-    const uint32_t p1 = r.sL + 1u + r.sT + r.sO + r.sK;
-    const uint32_t j = uint32_t(lane);
-    if (j < p1) {
-      uint32_t v;
-      if (j < r.sL) v = vbyte(r.uL, j, r.sL);
-      else if (j == r.sL) v = 0u;
-      else if (j < r.sL + 1u + r.sT) v = vbyte(r.uT, j - r.sL - 1u, r.sT);
-      else if (j < r.sL + 1u + r.sT + r.sO) v = vbyte(r.uO, j - r.sL - 1u - r.sT, r.sO);
-      else v = vbyte(r.uK, j - r.sL - 1u - r.sT - r.sO, r.sK);
-      p[j] = uint8_t(v);
-    }
-    p += p1;
-    const uint8_t *kp = m.arena + (r.kb ? m.key_off[msg] : 0);
-    for (uint32_t i = j; i < r.kb; i += 64) p[i] = kp[i];  // Key (:734)
-    p += r.kb;
-    if (j < r.sV) p[j] = uint8_t(vbyte(r.uV, j, r.sV));    // ValueLen (:738)
-    p += r.sV;
-    const uint8_t *vp = m.arena + (r.vb ? m.val_off[msg] : 0);
-    for (uint32_t i = j; i < r.vb; i += 64) p[i] = vp[i];  // Value (:741)
-    p += r.vb;
-    if (j < r.sH) p[j] = uint8_t(vbyte(r.uH, j, r.sH));    // HeaderCount (:745)
-    p += r.sH;
-    const uint8_t *hp = m.arena + (r.hb ? m.hdr_off[msg] : 0);
-    for (uint32_t i = j; i < r.hb; i += 64) p[i] = hp[i];  // Headers (:748)
-  }
-  // MaxTimestamp: block max
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const int64_t y = __shfl_xor(mx, d);
-    mx = y > mx ? y : mx;
-  }
-  if (lane == 0) wmax[w] = mx;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t M = 0;
-    for (int i = 0; i < kWaves; ++i) M = wmax[i] > M ? wmax[i] : M;
-    const uint32_t size = batch_sizes[blockIdx.x];
+  const Batch b = batches[blockIdx.y];
+  uint8_t *bo = out + out_offs[blockIdx.y];
+  const uint32_t k = blockIdx.x * kRecBlock + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t base_ts = b.msg_count ? m.ts[b.first_msg] : 0;
     st_be(bo + 0, 0, 8);                                   // BaseOffset (:362)
-    st_be(bo + 8, size - 12u, 4);                          // Length (:1265)
+    st_be(bo + 8, batch_sizes[blockIdx.y] - 12u, 4);       // Length (:1265)
     st_be(bo + 12, 0, 4);                                  // PartitionLeaderEpoch (:368)
     bo[16] = 2;                                            // Magic (:371)
     st_be(bo + 17, 0, 4);                                  // CRC: calc_crc_v2 later
     st_be(bo + 21, uint16_t(b.attributes), 2);             // Attributes (:1271)
     st_be(bo + 23, uint32_t(b.msg_count - 1u), 4);         // LastOffsetDelta (:1275)
     st_be(bo + 27, uint64_t(base_ts), 8);                  // BaseTimestamp (:1279)
-    st_be(bo + 35, uint64_t(M), 8);                        // MaxTimestamp (:1283)
+    st_be(bo + 35, uint64_t(max_ts[blockIdx.y]), 8);       // MaxTimestamp (:1283)
     st_be(bo + 43, uint64_t(b.producer_id), 8);            // ProducerId (:392)
     st_be(bo + 51, uint16_t(b.producer_epoch), 2);         // ProducerEpoch (:395)
     st_be(bo + 53, uint32_t(b.base_sequence), 4);          // BaseSequence (:1287)
     st_be(bo + 57, b.msg_count, 4);                        // RecordCount (:1291)
   }
+  if (k >= b.msg_count) return;
+  const uint32_t msg = b.first_msg + k;
+  const Rec r = rec_fields(m, msg, k, m.ts[b.first_msg]);
+  uint8_t *p = bo + rec_offs[msg];
+  // Length, Attributes (0), TimestampDelta, OffsetDelta, KeyLen (:717-731)
+  const uint32_t p1 = r.sL + 1u + r.sT + r.sO + r.sK;
+  for (uint32_t j = 0; j < p1; ++j) {
+    uint32_t v;
+    if (j < r.sL) v = vbyte(r.uL, j, r.sL);
+    else if (j == r.sL) v = 0u;
+    else if (j < r.sL + 1u + r.sT) v = vbyte(r.uT, j - r.sL - 1u, r.sT);
+    else if (j < r.sL + 1u + r.sT + r.sO) v = vbyte(r.uO, j - r.sL - 1u - r.sT, r.sO);
+    else v = vbyte(r.uK, j - r.sL - 1u - r.sT - r.sO, r.sK);
+    p[j] = uint8_t(v);
+  }
+  p += p1;
+  copy_bytes(p, m.arena + (r.kb ? m.key_off[msg] : 0), r.kb);  // Key (:734)
+  p += r.kb;
+  for (uint32_t j = 0; j < r.sV; ++j) p[j] = uint8_t(vbyte(r.uV, j, r.sV));  // ValueLen (:738)
+  p += r.sV;
+  copy_bytes(p, m.arena + (r.vb ? m.val_off[msg] : 0), r.vb);  // Value (:741)
+  p += r.vb;
+  for (uint32_t j = 0; j < r.sH; ++j) p[j] = uint8_t(vbyte(r.uH, j, r.sH));  // HeaderCount (:745)
+  p += r.sH;
+  copy_bytes(p, m.arena + (r.hb ? m.hdr_off[msg] : 0), r.hb);  // Headers (:748)
 }
 
 }  // namespace rdk
@@ -223,35 +275,69 @@ static Msgs to_msgs(const rdk_hip_msgs_t *m) {
   return r;
 }
 
-RDK_API int rdk_hip_msgset_v2_sizes(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *d_batches,
+// host batch descriptors -> a device copy on the stream; returns the chunk count
+static int upload_batches(const rdk_hip_v2_batch_t *batches, uint32_t n, hipStream_t s,
+                          Batch **d, uint32_t *nchunk) {
+  uint32_t mx = 1;
+  for (uint32_t i = 0; i < n; ++i) mx = batches[i].msg_count > mx ? batches[i].msg_count : mx;
+  *nchunk = (mx + kRecBlock - 1) / kRecBlock;
+  RDK_HIP_CHECK(hipMallocAsync(reinterpret_cast<void **>(d), size_t(n) * sizeof(Batch), s));
+  RDK_HIP_CHECK(hipMemcpyAsync(*d, batches, size_t(n) * sizeof(Batch), hipMemcpyHostToDevice, s));
+  return 0;
+}
+
+RDK_API int rdk_hip_msgset_v2_sizes(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *batches,
                                     uint32_t n, uint32_t *d_rec_offs, uint32_t *d_batch_sizes,
+                                    int64_t *d_max_ts, void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!msgs_ok(msgs) || !batches || !d_rec_offs || !d_batch_sizes || !d_max_ts)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Batch *db = nullptr;
+  uint32_t nchunk = 0;
+  int rc = upload_batches(batches, n, s, &db, &nchunk);
+  if (rc) return rc;
+  uint32_t *tot = nullptr;
+  int64_t *cmax = nullptr;
+  const size_t nc = size_t(n) * nchunk;
+  RDK_HIP_CHECK(hipMallocAsync(reinterpret_cast<void **>(&tot), nc * 4, s));
+  RDK_HIP_CHECK(hipMallocAsync(reinterpret_cast<void **>(&cmax), nc * 8, s));
+  const Msgs m = to_msgs(msgs);
+  hipLaunchKernelGGL(v2_chunk_kernel, dim3(nchunk, n), dim3(kRecBlock), 0, s, m, db, nchunk,
+                     d_rec_offs, tot, cmax);
+  hipLaunchKernelGGL(v2_batch_kernel, dim3(n), dim3(64), 0, s, nchunk, tot, cmax, d_batch_sizes,
+                     d_max_ts);
+  hipLaunchKernelGGL(v2_fixup_kernel, dim3(nchunk, n), dim3(kRecBlock), 0, s, db, nchunk, tot,
+                     d_rec_offs);
+  RDK_HIP_CHECK(hipGetLastError());
+  RDK_HIP_CHECK(hipFreeAsync(tot, s));
+  RDK_HIP_CHECK(hipFreeAsync(cmax, s));
+  RDK_HIP_CHECK(hipFreeAsync(db, s));
+  return RDK_HIP_OK;
+}
+
+RDK_API int rdk_hip_msgset_v2_write(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *batches,
+                                    uint32_t n, const uint32_t *d_rec_offs,
+                                    const uint32_t *d_batch_sizes, const int64_t *d_max_ts,
+                                    const uint64_t *d_out_offs, uint8_t *d_out, uint32_t *d_crc,
                                     void *stream) {
   Ctx *c = ctx();
   if (!c) return RDK_HIP_E_NODEV;
   if (!n) return RDK_HIP_OK;
-  if (!msgs_ok(msgs) || !d_batches || !d_rec_offs || !d_batch_sizes)
-    return set_error(RDK_HIP_E_INVAL, "null pointer");
-  hipLaunchKernelGGL(v2_sizes_kernel, dim3(n), dim3(kRecBlock), 0, static_cast<hipStream_t>(stream),
-                     to_msgs(msgs), reinterpret_cast<const Batch *>(d_batches), d_rec_offs,
-                     d_batch_sizes);
-  RDK_HIP_CHECK(hipGetLastError());
-  return RDK_HIP_OK;
-}
-
-RDK_API int rdk_hip_msgset_v2_write(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t *d_batches,
-                                    uint32_t n, const uint32_t *d_rec_offs,
-                                    const uint32_t *d_batch_sizes, const uint64_t *d_out_offs,
-                                    uint8_t *d_out, uint32_t *d_crc, void *stream) {
-  Ctx *c = ctx();
-  if (!c) return RDK_HIP_E_NODEV;
-  if (!n) return RDK_HIP_OK;
-  if (!msgs_ok(msgs) || !d_batches || !d_rec_offs || !d_batch_sizes || !d_out_offs || !d_out)
+  if (!msgs_ok(msgs) || !batches || !d_rec_offs || !d_batch_sizes || !d_max_ts || !d_out_offs ||
+      !d_out)
     return set_error(RDK_HIP_E_INVAL, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(v2_write_kernel, dim3(n), dim3(kRecBlock), 0, s, to_msgs(msgs),
-                     reinterpret_cast<const Batch *>(d_batches), d_rec_offs, d_batch_sizes,
-                     d_out_offs, d_out);
+  Batch *db = nullptr;
+  uint32_t nchunk = 0;
+  int rc = upload_batches(batches, n, s, &db, &nchunk);
+  if (rc) return rc;
+  hipLaunchKernelGGL(v2_write_kernel, dim3(nchunk, n), dim3(kRecBlock), 0, s, to_msgs(msgs), db,
+                     d_rec_offs, d_batch_sizes, d_max_ts, d_out_offs, d_out);
   RDK_HIP_CHECK(hipGetLastError());
+  RDK_HIP_CHECK(hipFreeAsync(db, s));
   if (d_crc)  // calc_crc_v2 (:1229-1246): the batch size is its capacity
     return rdk_hip_msgset_v2_crc(d_out, d_out_offs, d_batch_sizes, d_crc, n,
                                  RDK_HIP_V2_CRC_FINALIZE, stream);

@@ -295,6 +295,56 @@ def bench_serialize(args, rank, world, n=None, per_batch=9500):
             "host_sample": (base, per_batch)}
 
 
+def bench_index(args, rank, world, n=None, per_batch=9500):
+    """the consumer's record index (rd_kafka_msgset_reader_msg_v2,
+    rdkafka_msgset_reader.c:715-927) over ~1 MiB MsgVersion 2 batches of ~100-byte JSON
+    records (built on the device by the record writer): one row per record with offset,
+    timestamp, key / value / headers positions."""
+    import numpy as np
+    import torch
+    import librdkafka_amd as L
+    n = n or args.partitions // world
+    base, d, _ = tiled_messages(n, per_batch, seed=42 + rank)
+    b = np.zeros(n, dtype=L.V2_BATCH_DTYPE)
+    b["first_msg"] = np.arange(n) * per_batch
+    b["msg_count"] = per_batch
+    out, offs, sizes, _ = L.msgset_v2_build(d, b, crc=True)
+    rec_offs = offs + 61
+    rec_lens = sizes - 61
+    row_offs = torch.arange(n, dtype=torch.int64, device="cuda") * per_batch
+    caps = torch.full((n,), per_batch, dtype=torch.int32, device="cuda")
+    rows = {k: torch.empty(n * per_batch, dtype=getattr(torch, t), device="cuda")
+            for k, t in L.V2_ROW_FIELDS}
+    cnt = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ms, kms = _timed(lambda: L.msgset_v2_index(out, offs, out, rec_offs, rec_lens, row_offs,
+                                               caps, rows, cnt), args.steps, args.warmup, world)
+    assert bool((cnt == per_batch).all())
+    total = int(rec_lens.to(torch.int64).sum())
+    return {"ms": ms, "kernel_ms": kms, "bytes": total, "records": n,
+            "alg_bytes": total + 61 * n + 40 * n * per_batch,
+            "host_sample": (base, per_batch)}
+
+
+def cpu_baseline_index(base, per_batch, seconds=3.0):
+    """The oracle restatement of rd_kafka_msgset_reader_msg_v2 (msgset_oracle.c), one host
+    thread, over a batch of the same messages."""
+    import oracle
+    per_batch = min(per_batch, 16384)
+    b = oracle.msgset_v2_write(base, 0, per_batch)
+    rec = b[61:]
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        n, _ = oracle.msgset_v2_index(rec, 0, 0, max_rows=per_batch)
+        assert n == per_batch
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(passes * len(rec) / el / 1e9, 3), "unit": "GB/s", "cores": 1,
+            "kind": "port", "sample": f"{passes} passes over {per_batch} JSON records "
+                                      f"({len(rec)} B), reader_msg_v2 restated, {cpu_model()}"}
+
+
 def cpu_baseline_serialize(base, per_batch, seconds=3.0):
     """The oracle restatement of rd_kafka_msgset_writer_write_msg_v2 + header finalize +
     calc_crc_v2 (msgset_oracle.c), one host thread, batches of the same messages."""
@@ -483,6 +533,13 @@ def leg_line(name, res, steps, world, cpu=None):
     return d
 
 
+def index_leg(rank, world, no_cpu):
+    res = bench_index(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
+    cpu = None if no_cpu else cpu_baseline_index(*res.pop("host_sample"))
+    res.pop("host_sample", None)
+    return leg_line("index", res, 3, world, cpu)
+
+
 def serialize_leg(rank, world, no_cpu):
     res = bench_serialize(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
     cpu = None if no_cpu else cpu_baseline_serialize(*res.pop("host_sample"))
@@ -518,7 +575,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="crc",
-                    choices=["crc", "lz4c", "lz4c_fast", "consumer", "producer", "serialize"])
+                    choices=["crc", "lz4c", "lz4c_fast", "consumer", "producer", "serialize",
+                             "index"])
     ap.add_argument("--batches", type=int, default=CRC_BATCHES)
     ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -543,6 +601,8 @@ def main():
             res = bench_producer(args, rank, world)
         elif args.workload == "serialize":
             res = bench_serialize(args, rank, world)
+        elif args.workload == "index":
+            res = bench_index(args, rank, world)
         else:
             res = bench_consumer(args, rank, world)
         t_max = max_over_ranks(res["ms"], world)
@@ -551,6 +611,8 @@ def main():
             if not args.no_cpu_baseline and world == 1:
                 if args.workload == "serialize":
                     cpu = cpu_baseline_serialize(*res["host_sample"])
+                elif args.workload == "index":
+                    cpu = cpu_baseline_index(*res["host_sample"])
                 else:
                     cpu = cpu_baseline_lz4("decompress" if args.workload == "consumer"
                                            else "compress")
@@ -617,6 +679,7 @@ def main():
                     "consumer", bench_consumer(argparse.Namespace(steps=3, warmup=1, partitions=1024),
                                                rank, world), 3, 1, cpu("decompress")),
                 "v2_record_serialize_1MiB_json": serialize_leg(rank, world, args.no_cpu_baseline),
+                "v2_record_index_1MiB_json": index_leg(rank, world, args.no_cpu_baseline),
                 "producer_pipeline_1MiB_json_pcie": leg_line(
                     "producer", bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512),
                                                rank, world), 2, 1, cpu("compress")),

@@ -226,6 +226,35 @@ int rdk_hip_msgset_v2_write(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t
                             const uint64_t *d_out_offs, uint8_t *d_out, uint32_t *d_crc,
                             void *stream);
 
+/* ---- MsgVersion 2 record index ------------------------------
+ * rd_kafka_msgset_reader_msg_v2 (rdkafka_msgset_reader.c:715-927) for every record of
+ * n batches, on the device: batch i's header (BaseOffset, BaseTimestamp) at
+ * d_hdr_base + d_hdr_offs[i], its (uncompressed / decompressed) records at
+ * d_rec_base + d_rec_offs[i], d_rec_lens[i] bytes.  Row j of batch i goes to
+ * index d_row_offs[i] + j of every rows array (at most d_row_caps[i] rows):
+ *   offset = BaseOffset + OffsetDelta (:742), timestamp = BaseTimestamp +
+ *   TimestampDelta (:911-912, CreateTime), key/value offset (from the records start)
+ *   and length (-1 = null), headers = HeaderCount varint + headers (binhdrs, :876-878).
+ * d_count[i] = number of records, or -(1+j) when record j fails to parse (the
+ * reader's rd_kafka_buf_parse_fail / underflow; fields overrunning the record's Length
+ * fail; varints longer than 10 bytes fail).  Control batches, aborted transactions and
+ * offsets below the fetch offset are the caller's (record-level filters of :744-865). */
+typedef struct rdk_hip_v2_rows_s {  /* device arrays */
+  int64_t *offset;
+  int64_t *timestamp;
+  uint32_t *key_off;
+  int32_t *key_len;
+  uint32_t *value_off;
+  int32_t *value_len;
+  uint32_t *headers_off;
+  uint32_t *headers_len;
+} rdk_hip_v2_rows_t;
+int rdk_hip_msgset_v2_index(const void *d_hdr_base, const uint64_t *d_hdr_offs,
+                            const void *d_rec_base, const uint64_t *d_rec_offs,
+                            const uint32_t *d_rec_lens, const uint64_t *d_row_offs,
+                            const uint32_t *d_row_caps, const rdk_hip_v2_rows_t *rows,
+                            int32_t *d_count, uint32_t n_batches, void *stream);
+
 /* Deterministic synthetic workloads generated on the device (bench/tests).
  * v2 batches: n batches of `batch_size` bytes at i*batch_size: a valid 61-byte
  * v2 header (Magic 2, Length = batch_size-12, RecordCount) followed by

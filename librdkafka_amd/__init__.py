@@ -50,6 +50,7 @@ EXPORTED_SYMBOLS = (
     "rdk_hip_gen_v2_batches", "rdk_hip_producer_new", "rdk_hip_producer_produce",
     "rdk_hip_producer_flush", "rdk_hip_producer_poll", "rdk_hip_producer_destroy",
     "rdk_hip_gen_json", "rdk_hip_msgset_v2_sizes", "rdk_hip_msgset_v2_write",
+    "rdk_hip_msgset_v2_index",
 )
 
 
@@ -119,6 +120,8 @@ def lib():
     L.rdk_hip_msgset_v2_sizes.argtypes = [C.POINTER(_Msgs), vp, u32, vp, vp, vp, vp]
     L.rdk_hip_msgset_v2_write.restype = i32
     L.rdk_hip_msgset_v2_write.argtypes = [C.POINTER(_Msgs), vp, u32, vp, vp, vp, vp, vp, vp, vp]
+    L.rdk_hip_msgset_v2_index.restype = i32
+    L.rdk_hip_msgset_v2_index.argtypes = [vp] * 7 + [C.POINTER(_Rows), vp, u32, vp]
     _lib = L
     return L
 
@@ -128,6 +131,18 @@ class _Msgs(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("arena", "timestamp", "key_off", "key_len", "value_off",
                                           "value_len", "headers_off", "headers_len",
                                           "header_count")]
+
+
+class _Rows(C.Structure):
+    """rdk_hip_v2_rows_t: device arrays of the record index."""
+    _fields_ = [(n, C.c_void_p) for n in ("offset", "timestamp", "key_off", "key_len",
+                                          "value_off", "value_len", "headers_off",
+                                          "headers_len")]
+
+
+V2_ROW_FIELDS = (("offset", "int64"), ("timestamp", "int64"), ("key_off", "int32"),
+                 ("key_len", "int32"), ("val_off", "int32"), ("val_len", "int32"),
+                 ("hdr_off", "int32"), ("hdr_len", "int32"))
 
 
 # rdk_hip_v2_batch_t
@@ -417,3 +432,16 @@ def msgset_v2_build(msgs: dict, batches: np.ndarray, crc: bool = True, stream=No
                                          _ptr(sizes), _ptr(max_ts), _ptr(offs), _ptr(out),
                                          _ptr(crcs), s), "msgset_v2_write")
     return out, offs, sizes[:n], (crcs[:n] if crc else None)
+
+
+def msgset_v2_index(hdr_base, hdr_offs, rec_base, rec_offs, rec_lens, row_offs, row_caps,
+                    rows: dict, count, stream=None) -> None:
+    """MsgVersion 2 record index on the device (rdkafka_msgset_reader.c:715-927): `rows`
+    holds cuda tensors named as V2_ROW_FIELDS; count[i] = records of batch i or
+    -(1+j) when record j fails to parse."""
+    r = _Rows(*(rows[k].data_ptr() for k, _ in V2_ROW_FIELDS))
+    _check(lib().rdk_hip_msgset_v2_index(_ptr(hdr_base), _ptr(hdr_offs), _ptr(rec_base),
+                                         _ptr(rec_offs), _ptr(rec_lens), _ptr(row_offs),
+                                         _ptr(row_caps), C.byref(r), _ptr(count),
+                                         int(hdr_offs.numel()), _stream(stream)),
+           "msgset_v2_index")

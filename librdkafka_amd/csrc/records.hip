@@ -8,6 +8,8 @@
 // with the batch loop semantics of write_msgq (:804-902): OffsetDelta = index in
 // the batch, TimestampDelta against the first message, MaxTimestamp from 0.
 //
+// Record index (rdkafka_msgset_reader.c:715-927): see v2_index_kernel.
+//
 // Workgroups of 256 threads work on chunks of 256 records (grid = chunks x batches):
 //   sizes: a thread sizes one record (zig-zag varints, rdvarint.h:48-75), a chunk scan
 //          plus a per-batch scan of chunk totals place it -> record offsets, batch size;
@@ -17,6 +19,8 @@
 #include <hip/hip_runtime.h>
 
 #include "common.h"
+
+#include <cstring>
 
 namespace rdk {
 
@@ -249,6 +253,251 @@ __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch
   copy_bytes(p, m.arena + (r.hb ? m.hdr_off[msg] : 0), r.hb);  // Headers (:748)
 }
 
+// ---- record index: rd_kafka_msgset_reader_msg_v2
+// (rdkafka_msgset_reader.c:715-927) for every record of a batch, one row each.
+// One wavefront per batch.  The records are staged through an 8 KiB LDS window (16-byte
+// buffer loads): lane 0 walks the Length chain (:736-737) over it -- one LDS round trip
+// per record --
+// and lists the records that lie wholly inside it; then every lane parses one listed
+// record's fields (:738-878) from LDS.  Records larger than the window are parsed by
+// lane 0 straight from global memory.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct Rows {  // rdk_hip_v2_rows_t
+  int64_t *offset, *timestamp;
+  uint32_t *key_off;
+  int32_t *key_len;
+  uint32_t *val_off;
+  int32_t *val_len;
+  uint32_t *hdr_off, *hdr_len;
+};
+
+constexpr uint32_t kIdxWin = 8192;            // LDS window per wavefront
+constexpr uint32_t kIdxList = kIdxWin / 6;    // a record is at least 6 bytes
+constexpr int kIdxWaves = 4;
+
+typedef __attribute__((address_space(3))) uint8_t lds_b;
+typedef __attribute__((address_space(3))) uint16_t lds_h;
+
+// zig-zag varint at p (rdvarint.h:114-141, rdbuf.c:877-912) with bytes [p, lim)
+// readable through get(); returns bytes read, 0 on underflow or more than 10 bytes
+template <class Get>
+__device__ __forceinline__ uint32_t idx_varint(Get get, uint32_t p, uint32_t lim, int64_t &v) {
+  uint64_t num = 0;
+  for (uint32_t k = 0; k < 10; ++k) {
+    if (p + k >= lim) return 0;
+    const uint32_t b = get(p + k);
+    num |= uint64_t(b & 0x7fu) << (7u * k);
+    if (!(b & 0x80u)) {
+      v = int64_t(num >> 1) ^ -int64_t(num & 1u);
+      return k + 1u;
+    }
+  }
+  return 0;
+}
+
+// fields of the record whose Length varint starts at r (positions through get(), all
+// below `lim`); false = parse failure (rd_kafka_buf_parse_fail / underflow)
+struct IdxRow {
+  int64_t tsd, od;
+  int32_t kl, vl;
+  uint32_t ko, vo, ho, hl;
+};
+template <class Get>
+__device__ __forceinline__ bool idx_record(Get get, uint32_t r, uint32_t lim, IdxRow &o,
+                                           uint32_t &next) {
+  int64_t L, kl, vl;
+  uint32_t n = idx_varint(get, r, lim, L);  // :736
+  if (!n) return false;
+  uint32_t p = r + n;
+  if (L < 0 || uint64_t(L) > uint64_t(lim - p)) return false;
+  const uint32_t end = p + uint32_t(L);     // :737
+  if (p + 1u > end) return false;
+  p += 1u;                                  // Attributes :738
+  if (!(n = idx_varint(get, p, end, o.tsd))) return false;  // :740
+  p += n;
+  if (!(n = idx_varint(get, p, end, o.od))) return false;   // :741
+  p += n;
+  if (!(n = idx_varint(get, p, end, kl))) return false;     // :871
+  p += n;
+  if (kl < -1 || (kl > 0 && uint64_t(kl) > uint64_t(end - p))) return false;
+  o.ko = p;
+  o.kl = int32_t(kl);
+  if (kl > 0) p += uint32_t(kl);
+  if (!(n = idx_varint(get, p, end, vl))) return false;     // :872
+  p += n;
+  if (vl < -1 || (vl > 0 && uint64_t(vl) > uint64_t(end - p))) return false;
+  o.vo = p;
+  o.vl = int32_t(vl);
+  if (vl > 0) p += uint32_t(vl);
+  o.ho = p;                                 // binhdrs: HeaderCount + headers, :876-878
+  o.hl = end - p;
+  next = end;
+  return true;
+}
+
+__device__ __forceinline__ int64_t ld_be64(const uint8_t *p) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
+  return int64_t(v);
+}
+
+__global__ __launch_bounds__(64 * kIdxWaves) void v2_index_kernel(
+    const uint8_t *__restrict__ hdr_base, const uint64_t *__restrict__ hdr_offs,
+    const uint8_t *__restrict__ rec_base, const uint64_t *__restrict__ rec_offs,
+    const uint32_t *__restrict__ rec_lens, const uint64_t *__restrict__ row_offs,
+    const uint32_t *__restrict__ row_caps, Rows rows, int32_t *__restrict__ count, uint32_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[kIdxWaves][kIdxWin + 32];
+  __shared__ uint16_t list_all[kIdxWaves][kIdxList];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t bi = blockIdx.x * kIdxWaves + uint32_t(wv);
+  if (bi >= n) return;
+  lds_b *win = (lds_b *)win_all[wv];
+  lds_h *list = (lds_h *)list_all[wv];
+  const uint8_t *hdr = hdr_base + hdr_offs[bi];
+  const int64_t base_off = ld_be64(hdr + 0);   // BaseOffset (msetr_v2_hdr, :742)
+  const int64_t base_ts = ld_be64(hdr + 27);   // BaseTimestamp (:911-912)
+  const uint8_t *rec = rec_base + rec_offs[bi];
+  const uint32_t len = rec_lens[bi];
+  const uint64_t row0 = row_offs[bi];
+  const uint32_t cap = row_caps[bi];
+  uint32_t pos = 0, nrow = 0;
+  int32_t err = -1;  // first failing record index
+  auto gget = [&](uint32_t p) -> uint32_t { return rec[p]; };
+  while (pos < len && err < 0) {
+    // stage [pos, pos + kIdxWin): 16-byte buffer loads from the 16-byte aligned address
+    // below, all issued before their LDS stores; bytes past the batch read as 0
+    const uint32_t base = pos, wl = len - base < kIdxWin ? len - base : kIdxWin;
+    const uintptr_t ga = reinterpret_cast<uintptr_t>(rec + base);
+    const uintptr_t al = ga & ~uintptr_t(15);
+    const uint32_t sh = uint32_t(ga - al);  // window byte q is LDS byte q + sh
+    // (range checks are per dword: round up so the batch's last bytes are read; the bytes
+    // after them in that dword share its page and are never used)
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(al), 0,
+                                                        int((sh + wl + 3u) & ~3u), 0x00020000);
+    {
+      constexpr int kV = int((kIdxWin + 16) / (64 * 16)) + 1;  // 16-byte vectors per lane
+      u32x4 v[kV];
+#pragma unroll
+      for (int it = 0; it < kV; ++it)
+        v[it] = __builtin_amdgcn_raw_buffer_load_b128(rs, uint32_t((lane + 64 * it) * 16), 0, 0);
+#pragma unroll
+      for (int it = 0; it < kV; ++it) {
+        const uint32_t o = uint32_t((lane + 64 * it) * 16);
+        if (o < kIdxWin + 16) *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(win + o) = v[it];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    auto lget = [&](uint32_t p) -> uint32_t { return win[p - base + sh]; };
+    // walk: records wholly inside the window go to the list
+    // the walk is wave-uniform: LDS bytes are read as broadcasts and moved to scalar
+    // registers, so its arithmetic runs on the scalar unit
+    uint32_t nl = 0, stop = pos;
+    int32_t werr = -1;
+    auto sget = [&](uint32_t p) -> uint32_t { return __builtin_amdgcn_readfirstlane(lget(p)); };
+    {
+      uint32_t p = pos;
+      const uint32_t wend = base + wl;
+      while (p < len && nl < kIdxList) {
+        int64_t L;
+        uint32_t sz;
+        // Length varints of this workload are 1-2 bytes: both bytes in one LDS round trip
+        const uint32_t b0 = sget(p), b1 = sget(p + 1u);
+        if (b0 < 0x80u && p + 1u <= wend) {
+          sz = 1u;
+          L = int64_t(b0 >> 1) ^ -int64_t(b0 & 1u);
+        } else if (b1 < 0x80u && p + 2u <= wend) {
+          const uint64_t u = (b0 & 0x7fu) | (uint64_t(b1) << 7);
+          sz = 2u;
+          L = int64_t(u >> 1) ^ -int64_t(u & 1u);
+        } else {
+          sz = idx_varint(sget, p, wend, L);
+        }
+        if (!sz) {
+          if (wend < len && p > base) break;  // varint cut by the window: next window
+          werr = 0;                           // underflow at the batch end (or huge varint)
+          break;
+        }
+        if (L < 0 || uint64_t(L) > uint64_t(len - p - sz)) { werr = 0; break; }
+        const uint32_t e = p + sz + uint32_t(L);
+        if (e > wend) break;  // ends past the window: next window (or the big path)
+        if (lane == 0) list[nl] = uint16_t(p - base);
+        ++nl;
+        p = e;
+      }
+      stop = p;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // parse the listed records, 64 at a time
+    int32_t bad = 0x7fffffff;
+    for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
+      const uint32_t i = i0 + uint32_t(lane);
+      if (i < nl) {
+        const uint32_t r = base + list[i];
+        IdxRow o;
+        uint32_t nx;
+        if (!idx_record(lget, r, base + wl, o, nx) || nrow + i >= cap) {
+          bad = int32_t(i) < bad ? int32_t(i) : bad;
+        } else {
+          const uint64_t row = row0 + nrow + i;
+          rows.offset[row] = base_off + o.od;        // :742
+          rows.timestamp[row] = base_ts + o.tsd;     // :911-912 (CreateTime)
+          rows.key_off[row] = o.ko;
+          rows.key_len[row] = o.kl;
+          rows.val_off[row] = o.vo;
+          rows.val_len[row] = o.vl;
+          rows.hdr_off[row] = o.ho;
+          rows.hdr_len[row] = o.hl;
+        }
+      }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const int32_t y = __shfl_xor(bad, d);
+      bad = y < bad ? y : bad;
+    }
+    if (bad != 0x7fffffff) {
+      err = int32_t(nrow) + bad;
+      break;
+    }
+    nrow += nl;
+    if (werr >= 0) {
+      err = int32_t(nrow);
+      break;
+    }
+    pos = stop;
+    if (nl == 0 && pos < len) {
+      // a record larger than the window (or whose Length varint is cut at the batch
+      // end): lane 0 parses it from global memory
+      IdxRow o;
+      uint32_t nx = pos;
+      bool ok = false;
+      if (lane == 0) ok = idx_record(gget, pos, len, o, nx) && nrow < cap;
+      ok = __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
+      nx = __builtin_amdgcn_readfirstlane(nx);
+      if (!ok) {
+        err = int32_t(nrow);
+        break;
+      }
+      if (lane == 0) {
+        const uint64_t row = row0 + nrow;
+        rows.offset[row] = base_off + o.od;
+        rows.timestamp[row] = base_ts + o.tsd;
+        rows.key_off[row] = o.ko;
+        rows.key_len[row] = o.kl;
+        rows.val_off[row] = o.vo;
+        rows.val_len[row] = o.vl;
+        rows.hdr_off[row] = o.ho;
+        rows.hdr_len[row] = o.hl;
+      }
+      nrow += 1;
+      pos = nx;
+    }
+  }
+  if (lane == 0) count[bi] = err >= 0 ? -(1 + err) : int32_t(nrow);
+}
+
 }  // namespace rdk
 
 using namespace rdk;
@@ -341,5 +590,31 @@ RDK_API int rdk_hip_msgset_v2_write(const rdk_hip_msgs_t *msgs, const rdk_hip_v2
   if (d_crc)  // calc_crc_v2 (:1229-1246): the batch size is its capacity
     return rdk_hip_msgset_v2_crc(d_out, d_out_offs, d_batch_sizes, d_crc, n,
                                  RDK_HIP_V2_CRC_FINALIZE, stream);
+  return RDK_HIP_OK;
+}
+
+static_assert(sizeof(rdk_hip_v2_rows_t) == sizeof(Rows), "rdk_hip_v2_rows_t layout");
+
+RDK_API int rdk_hip_msgset_v2_index(const void *d_hdr_base, const uint64_t *d_hdr_offs,
+                                    const void *d_rec_base, const uint64_t *d_rec_offs,
+                                    const uint32_t *d_rec_lens, const uint64_t *d_row_offs,
+                                    const uint32_t *d_row_caps, const rdk_hip_v2_rows_t *rows,
+                                    int32_t *d_count, uint32_t n, void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_hdr_base || !d_hdr_offs || !d_rec_base || !d_rec_offs || !d_rec_lens || !d_row_offs ||
+      !d_row_caps || !rows || !rows->offset || !rows->timestamp || !rows->key_off ||
+      !rows->key_len || !rows->value_off || !rows->value_len || !rows->headers_off ||
+      !rows->headers_len || !d_count)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  Rows r;
+  std::memcpy(&r, rows, sizeof r);
+  hipLaunchKernelGGL(v2_index_kernel, dim3((n + kIdxWaves - 1) / kIdxWaves), dim3(64 * kIdxWaves),
+                     0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t *>(d_hdr_base), d_hdr_offs,
+                     static_cast<const uint8_t *>(d_rec_base), d_rec_offs, d_rec_lens, d_row_offs,
+                     d_row_caps, r, d_count, n);
+  RDK_HIP_CHECK(hipGetLastError());
   return RDK_HIP_OK;
 }

@@ -53,3 +53,67 @@ def test_v2_build_then_verify(engine):
     st = torch.zeros(len(spec), dtype=torch.int32, device="cuda")
     E.msgset_v2_crc(out, offs, sizes, st, E.V2_CRC_VERIFY)
     assert int(st.abs().sum()) == 0
+
+
+def _index(engine, batches_bytes, rec_lens=None, caps=None):
+    """Index host-built v2 batches on the GPU; returns (count, rows) on the host."""
+    import torch
+    blob = b"".join(batches_bytes)
+    offs = np.cumsum([0] + [len(b) for b in batches_bytes[:-1]]).astype(np.int64)
+    lens = np.array([len(b) - 61 for b in batches_bytes], np.int64)
+    if rec_lens is not None:
+        lens = np.array(rec_lens, np.int64)
+    dev = torch.frombuffer(bytearray(blob + b"\0" * 64), dtype=torch.uint8).cuda()
+    n = len(batches_bytes)
+    nrows = [max(1, int(l) // 6 + 1) for l in lens]
+    if caps is None:
+        caps = nrows
+    row_offs = np.cumsum([0] + nrows[:-1]).astype(np.int64)
+    tot = int(sum(nrows))
+    rows = {k: torch.zeros(tot, dtype=getattr(torch, t), device="cuda")
+            for k, t in E.V2_ROW_FIELDS}
+    cnt = torch.zeros(n, dtype=torch.int32, device="cuda")
+    t = lambda a, dt: torch.from_numpy(np.asarray(a, dtype=dt)).cuda()  # noqa: E731
+    E.msgset_v2_index(dev, t(offs, np.int64), dev, t(offs + 61, np.int64), t(lens, np.int32),
+                      t(row_offs, np.int64), t(caps, np.int32), rows, cnt)
+    host = {k: v.cpu().numpy() for k, v in rows.items()}
+    return cnt.cpu().numpy(), host, row_offs
+
+
+def _check_index(oracle_mod, b, cnt, host, r0, rec_len=None):
+    import struct
+    rec = b[61:61 + (rec_len if rec_len is not None else len(b) - 61)]
+    bo, bts = struct.unpack(">q", b[:8])[0], struct.unpack(">q", b[27:35])[0]
+    n, exp = oracle_mod.msgset_v2_index(rec, bo, bts)
+    assert cnt == n, (cnt, n)
+    for k in exp:
+        assert (host[k][r0:r0 + max(n, 0)].astype(np.int64) ==
+                exp[k].astype(np.int64)).all(), k
+
+
+def test_v2_index_matches_oracle(engine, oracle_mod):
+    m = W.gen_messages(6000, seed=11)
+    spec = [(0, 1), (1, 500), (501, 2000), (2501, 3499)]
+    bs = [oracle_mod.msgset_v2_write(m, f, c, 5, 1, 0, 0) for f, c in spec]
+    bs[2] = bs[2][:8] + bytes(8) + bs[2][16:]  # header BaseOffset stays 0; arbitrary
+    cnt, host, r0 = _index(engine, bs)
+    for i, b in enumerate(bs):
+        _check_index(oracle_mod, b, cnt[i], host, r0[i])
+
+
+def test_v2_index_big_records_and_errors(engine, oracle_mod):
+    m = W.gen_messages(40, seed=5)
+    # one 20 KiB value (larger than the 8 KiB LDS window)
+    big = np.frombuffer(bytes(range(256)) * 80, np.uint8)
+    m["val_off"][7] = len(m["arena"]); m["val_len"][7] = len(big)
+    m["arena"] = np.concatenate([m["arena"], big])
+    ok = oracle_mod.msgset_v2_write(m, 0, 40)
+    trunc = ok[:-5]                                    # last record cut short
+    bad_len = bytearray(ok); bad_len[61] |= 0x80       # first Length varint runs on
+    bad_len = bytes(bad_len)
+    empty = oracle_mod.msgset_v2_write(m, 0, 1)[:61]   # no records at all
+    bs = [ok, trunc, bad_len, empty, ok]
+    cnt, host, r0 = _index(engine, bs, caps=[1000, 1000, 1000, 1, 10])
+    for i in range(4):
+        _check_index(oracle_mod, bs[i], cnt[i], host, r0[i])
+    assert cnt[4] == -(1 + 10)                          # row capacity 10: record 10 fails

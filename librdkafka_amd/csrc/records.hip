@@ -13,9 +13,8 @@
 // Workgroups of 256 threads work on chunks of 256 records (grid = chunks x batches):
 //   sizes: a thread sizes one record (zig-zag varints, rdvarint.h:48-75), a chunk scan
 //          plus a per-batch scan of chunk totals place it -> record offsets, batch size;
-//   write: one lane per record (256 records of a batch in flight per workgroup): the
-//          varint prefix bytes, then key / value / header bytes 16 loads ahead of their
-//          stores; thread 0 writes the header.
+//   write: per chunk, record descriptors in LDS, then output-centric 16-byte pieces:
+//          coalesced aligned stores, 16 arena loads in flight per lane (v2_write_kernel).
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -187,29 +186,46 @@ __device__ __forceinline__ void st_be(uint8_t *p, uint64_t v, int n) {
   for (int i = 0; i < n; ++i) p[i] = uint8_t(v >> (8 * (n - 1 - i)));
 }
 
-// n bytes src -> dst, 16 at a time: all loads of a round first (clamped to the last
-// byte, so always in bounds), then the stores
-__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n) {
-  for (uint32_t i = 0; i < n; i += 16) {
-    uint8_t t[16];
-#pragma unroll
-    for (uint32_t u = 0; u < 16; ++u) t[u] = src[(i + u < n) ? i + u : n - 1u];
-#pragma unroll
-    for (uint32_t u = 0; u < 16; ++u)
-      if (i + u < n) dst[i + u] = t[u];
-  }
+// ---- write: grid (chunks, batches); chunk 0 also writes the header.
+// Phase 1, one lane per record: field widths and sources into LDS.  Phase 2, output-centric:
+// the chunk's output span is cut into 16-byte pieces aligned in the batch; a lane builds a
+// piece byte by byte (the record by a binary search of the chunk's record offsets, then the
+// field: varint byte, Attributes, or an arena byte -- every piece issues its 16 arena loads
+// at once) and writes it with one 16-byte store, coalesced across the wave.  Pieces cut by
+// the span ends (shared with the neighbouring chunk or the header) use byte stores.
+struct RecD {
+  uint64_t u[6];      // zig-zag values: L, T, O, K, V, H
+  uint64_t src[3];    // arena offsets: key, value, headers
+  uint32_t off;       // record start from the batch start
+  uint32_t end[10];   // field ends from the record start: L, attr, T, O, K, key, V, val, H, hdrs
+};
+
+__device__ __forceinline__ uint32_t piece_byte(const RecD &d, uint32_t t, uint64_t &src) {
+  // returns the byte value, or 0x100 when the byte is arena[src]
+  if (t < d.end[0]) return vbyte(d.u[0], t, d.end[0]);
+  if (t < d.end[1]) return 0u;  // Attributes (:722)
+  if (t < d.end[2]) return vbyte(d.u[1], t - d.end[1], d.end[2] - d.end[1]);
+  if (t < d.end[3]) return vbyte(d.u[2], t - d.end[2], d.end[3] - d.end[2]);
+  if (t < d.end[4]) return vbyte(d.u[3], t - d.end[3], d.end[4] - d.end[3]);
+  if (t < d.end[5]) { src = d.src[0] + (t - d.end[4]); return 0x100u; }
+  if (t < d.end[6]) return vbyte(d.u[4], t - d.end[5], d.end[6] - d.end[5]);
+  if (t < d.end[7]) { src = d.src[1] + (t - d.end[6]); return 0x100u; }
+  if (t < d.end[8]) return vbyte(d.u[5], t - d.end[7], d.end[8] - d.end[7]);
+  src = d.src[2] + (t - d.end[8]);
+  return 0x100u;
 }
 
-// ---- write: one lane per record, grid (chunks, batches); chunk 0 also writes the header
 __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch *__restrict__ batches,
                                                             const uint32_t *__restrict__ rec_offs,
                                                             const uint32_t *__restrict__ batch_sizes,
                                                             const int64_t *__restrict__ max_ts,
                                                             const uint64_t *__restrict__ out_offs,
                                                             uint8_t *__restrict__ out) {
+  __shared__ RecD D[kRecBlock];
+  __shared__ uint32_t span[2];
   const Batch b = batches[blockIdx.y];
   uint8_t *bo = out + out_offs[blockIdx.y];
-  const uint32_t k = blockIdx.x * kRecBlock + threadIdx.x;
+  const uint32_t c0 = blockIdx.x * kRecBlock;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const int64_t base_ts = b.msg_count ? m.ts[b.first_msg] : 0;
     st_be(bo + 0, 0, 8);                                   // BaseOffset (:362)
@@ -226,31 +242,80 @@ __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch
     st_be(bo + 53, uint32_t(b.base_sequence), 4);          // BaseSequence (:1287)
     st_be(bo + 57, b.msg_count, 4);                        // RecordCount (:1291)
   }
-  if (k >= b.msg_count) return;
-  const uint32_t msg = b.first_msg + k;
-  const Rec r = rec_fields(m, msg, k, m.ts[b.first_msg]);
-  uint8_t *p = bo + rec_offs[msg];
-  // Length, Attributes (0), TimestampDelta, OffsetDelta, KeyLen (:717-731)
-  const uint32_t p1 = r.sL + 1u + r.sT + r.sO + r.sK;
-  for (uint32_t j = 0; j < p1; ++j) {
-    uint32_t v;
-    if (j < r.sL) v = vbyte(r.uL, j, r.sL);
-    else if (j == r.sL) v = 0u;
-    else if (j < r.sL + 1u + r.sT) v = vbyte(r.uT, j - r.sL - 1u, r.sT);
-    else if (j < r.sL + 1u + r.sT + r.sO) v = vbyte(r.uO, j - r.sL - 1u - r.sT, r.sO);
-    else v = vbyte(r.uK, j - r.sL - 1u - r.sT - r.sO, r.sK);
-    p[j] = uint8_t(v);
+  if (c0 >= b.msg_count) return;
+  const uint32_t nrec = b.msg_count - c0 < kRecBlock ? b.msg_count - c0 : kRecBlock;
+  // phase 1
+  if (threadIdx.x < nrec) {
+    const uint32_t k = c0 + threadIdx.x, msg = b.first_msg + k;
+    const Rec r = rec_fields(m, msg, k, m.ts[b.first_msg]);
+    RecD &d = D[threadIdx.x];
+    d.u[0] = r.uL; d.u[1] = r.uT; d.u[2] = r.uO; d.u[3] = r.uK; d.u[4] = r.uV; d.u[5] = r.uH;
+    d.src[0] = r.kb ? m.key_off[msg] : 0;
+    d.src[1] = r.vb ? m.val_off[msg] : 0;
+    d.src[2] = r.hb ? m.hdr_off[msg] : 0;
+    const uint32_t off = rec_offs[msg];
+    d.off = off;
+    uint32_t e = r.sL;
+    d.end[0] = e;
+    d.end[1] = e += 1u;
+    d.end[2] = e += r.sT;
+    d.end[3] = e += r.sO;
+    d.end[4] = e += r.sK;
+    d.end[5] = e += r.kb;
+    d.end[6] = e += r.sV;
+    d.end[7] = e += r.vb;
+    d.end[8] = e += r.sH;
+    d.end[9] = e += r.hb;
+    if (threadIdx.x == 0) span[0] = off;
+    if (threadIdx.x == nrec - 1u) span[1] = off + e;
   }
-  p += p1;
-  copy_bytes(p, m.arena + (r.kb ? m.key_off[msg] : 0), r.kb);  // Key (:734)
-  p += r.kb;
-  for (uint32_t j = 0; j < r.sV; ++j) p[j] = uint8_t(vbyte(r.uV, j, r.sV));  // ValueLen (:738)
-  p += r.sV;
-  copy_bytes(p, m.arena + (r.vb ? m.val_off[msg] : 0), r.vb);  // Value (:741)
-  p += r.vb;
-  for (uint32_t j = 0; j < r.sH; ++j) p[j] = uint8_t(vbyte(r.uH, j, r.sH));  // HeaderCount (:745)
-  p += r.sH;
-  copy_bytes(p, m.arena + (r.hb ? m.hdr_off[msg] : 0), r.hb);  // Headers (:748)
+  __syncthreads();
+  // phase 2
+  const uint32_t s0 = span[0], s1 = span[1];
+  // pieces are 16-byte aligned in memory (batch offsets are arbitrary)
+  const uint32_t q0 = s0 - uint32_t((reinterpret_cast<uintptr_t>(bo) + s0) & 15u);
+  for (uint32_t q = q0 + threadIdx.x * 16u; q < s1; q += kRecBlock * 16u) {
+    // record holding byte q (or the first record when q < s0)
+    uint32_t lo = 0, hi = nrec - 1u;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1u) >> 1;
+      if (D[mid].off <= q) lo = mid; else hi = mid - 1u;
+    }
+    uint32_t r = lo;
+    RecD dr = D[r];  // the current record's descriptor, in registers
+    uint32_t nxt = r + 1u < nrec ? D[r + 1u].off : 0xffffffffu;
+    uint32_t val[16];
+    uint64_t src[16];
+#pragma unroll
+    for (uint32_t u = 0; u < 16; ++u) {
+      const uint32_t p = q + u;
+      if (p >= nxt) {  // next record (records are >= 6 bytes: at most 3 per piece)
+        ++r;
+        dr = D[r];
+        nxt = r + 1u < nrec ? D[r + 1u].off : 0xffffffffu;
+      }
+      src[u] = 0;
+      val[u] = (p >= s0 && p < s1) ? piece_byte(dr, p - dr.off, src[u]) : 0x200u;
+    }
+    uint8_t byte[16];
+#pragma unroll
+    for (uint32_t u = 0; u < 16; ++u) byte[u] = m.arena[src[u]];  // all 16 loads in flight
+    uint32_t w[4] = {0, 0, 0, 0};
+    bool full = true;
+#pragma unroll
+    for (uint32_t u = 0; u < 16; ++u) {
+      const uint32_t v = val[u] == 0x100u ? uint32_t(byte[u]) : val[u];
+      full = full && val[u] != 0x200u;
+      w[u >> 2] |= (v & 0xffu) << (8u * (u & 3u));
+    }
+    if (full) {
+      *reinterpret_cast<uint4 *>(bo + q) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+#pragma unroll
+      for (uint32_t u = 0; u < 16; ++u)
+        if (val[u] != 0x200u) bo[q + u] = uint8_t(w[u >> 2] >> (8u * (u & 3u)));
+    }
+  }
 }
 
 // ---- record index: rd_kafka_msgset_reader_msg_v2

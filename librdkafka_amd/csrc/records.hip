@@ -415,7 +415,9 @@ __global__ __launch_bounds__(64 * kIdxWaves) void v2_index_kernel(
     const uint32_t *__restrict__ row_caps, Rows rows, int32_t *__restrict__ count, uint32_t n) {
   __shared__ __attribute__((aligned(16))) uint8_t win_all[kIdxWaves][kIdxWin + 32];
   __shared__ uint16_t list_all[kIdxWaves][kIdxList];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wave index through readfirstlane: the compiler then knows everything derived from the
+  // batch (pointers, lengths, the Length walk) is wave-uniform and keeps it scalar
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t bi = blockIdx.x * kIdxWaves + uint32_t(wv);
   if (bi >= n) return;
   lds_b *win = (lds_b *)win_all[wv];
@@ -522,6 +524,7 @@ __global__ __launch_bounds__(64 * kIdxWaves) void v2_index_kernel(
       const int32_t y = __shfl_xor(bad, d);
       bad = y < bad ? y : bad;
     }
+    bad = __builtin_amdgcn_readfirstlane(bad);  // uniform after the reduction
     if (bad != 0x7fffffff) {
       err = int32_t(nrow) + bad;
       break;

@@ -108,9 +108,14 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4v lds_u32x4;
 typedef __attribute__((address_space(1))) u32x4v g_u32x4;
-constexpr uint32_t kRing = 8192;
+#ifndef RDK_DEC_RING
+#define RDK_DEC_RING 4096
+#endif
+constexpr uint32_t kRing = RDK_DEC_RING;        // LDS history per wavefront (>= 4096, see
+                                                // lz4_decode_fast.h far-history note)
+static_assert(kRing >= 4096 && (kRing & (kRing - 1)) == 0, "ring size");
 constexpr uint32_t kRingMask = kRing - 1u;
-constexpr uint32_t kFlush = 4096;               // bytes per streamed piece
+constexpr uint32_t kFlush = kRing / 2 < 4096 ? kRing / 2 : 4096;  // bytes per streamed piece
 constexpr uint32_t kRingReach = kRing - 256u;   // max offset served from LDS
 constexpr int kDecWaves = 4;                    // wavefronts per workgroup
 
@@ -634,9 +639,13 @@ int lz4f_decompress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_off
   RDK_HIP_CHECK(hipMemsetAsync(work_count, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(lz4f_walk_kernel, dim3((n + 63) / 64), dim3(64), 0, s, d_in, d_in_offs,
                      d_in_lens, n, fs, bd, work_count, work);
-  // persistent grid: LDS (kDecWaves rings of 8 KiB) allows 5 workgroups per CU
+  // persistent grid: as many workgroups per CU as the LDS rings and the 32 wave slots allow
+  constexpr unsigned kWgPerCu = (160u * 1024u) / (kDecWaves * (kRing + 64u)) < 32u / kDecWaves
+                                    ? (160u * 1024u) / (kDecWaves * (kRing + 64u))
+                                    : 32u / kDecWaves;
   const uint64_t want = (uint64_t(n) * kMaxDesc + kDecWaves - 1) / kDecWaves;
-  const unsigned bgrid = unsigned(want < 1280u ? (want ? want : 1u) : 1280u);
+  const unsigned cap = 256u * kWgPerCu;
+  const unsigned bgrid = unsigned(want < cap ? (want ? want : 1u) : cap);
   hipLaunchKernelGGL(lz4f_blocks_kernel, dim3(bgrid), dim3(64 * kDecWaves), 0, s, d_in,
                      d_in_offs, d_out, d_out_offs, d_out_caps, n, fs, bd, work_count, work);
   hipLaunchKernelGGL(lz4f_seq_kernel, dim3(grid_waves(n, 4)), dim3(256), 0, s, d_in, d_in_offs,

@@ -74,6 +74,7 @@ struct Slot {
   hipStream_t s = nullptr;
   hipEvent_t done = nullptr;
   uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+  uint8_t *dh_out = nullptr;  // h_out as seen by the device (the pack kernel writes it)
   uint8_t *h_meta = nullptr, *d_meta = nullptr;
   size_t in_used = 0, out_used = 0;
   uint32_t nb = 0, polled = 0;
@@ -101,27 +102,55 @@ struct rdk_hip_producer_s {
 namespace {
 
 // per-slot batch table (pinned host + device mirror), arrays of B entries:
-//   rec_offs, out_offs, frame_offs (u64) | caps, rec_lens, frame_lens,
-//   batch_lens, crcs (u32)
+//   rec_offs, out_offs, frame_offs, pack_offs (u64) | caps, rec_lens, frame_lens,
+//   batch_lens, crcs (u32); then the pack cursor (u64)
 struct Meta {
-  uint64_t *rec_offs, *out_offs, *frame_offs;
+  uint64_t *rec_offs, *out_offs, *frame_offs, *pack_offs;
   uint32_t *caps, *rec_lens, *frame_lens, *batch_lens, *crcs;
+  unsigned long long *cursor;
 };
 Meta meta_at(uint8_t *base, uint32_t B) {
   Meta m;
   m.rec_offs = reinterpret_cast<uint64_t *>(base);
   m.out_offs = m.rec_offs + B;
   m.frame_offs = m.out_offs + B;
-  m.caps = reinterpret_cast<uint32_t *>(m.frame_offs + B);
+  m.pack_offs = m.frame_offs + B;
+  m.caps = reinterpret_cast<uint32_t *>(m.pack_offs + B);
   m.rec_lens = m.caps + B;
   m.frame_lens = m.rec_lens + B;
   m.batch_lens = m.frame_lens + B;
   m.crcs = m.batch_lens + B;
+  m.cursor = reinterpret_cast<unsigned long long *>(
+      (reinterpret_cast<uintptr_t>(m.crcs + B) + 7) & ~uintptr_t(7));
   return m;
 }
-size_t meta_bytes(uint32_t B) { return size_t(B) * (3 * 8 + 5 * 4); }
+size_t meta_bytes(uint32_t B) { return size_t(B) * (4 * 8 + 5 * 4) + 16; }
 
 size_t out_span(size_t len) { return (kV2Hdr + lz4f_compress_bound(len) + 255) & ~size_t(255); }
+
+// Finished batches -> the slot's pinned host buffer, packed back to back (16-byte aligned,
+// in completion order of an atomic cursor) by the GPU itself: only the batches' own bytes
+// cross PCIe, not the compress-bound slots of d_out.  One workgroup per batch.
+__global__ __launch_bounds__(256) void pack_to_host_kernel(const uint8_t *__restrict__ d_out,
+                                                          const uint64_t *__restrict__ out_offs,
+                                                          const uint32_t *__restrict__ batch_lens,
+                                                          uint32_t n, uint8_t *__restrict__ h_out,
+                                                          uint64_t *__restrict__ pack_offs,
+                                                          unsigned long long *__restrict__ cursor) {
+  __shared__ uint64_t at;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t len = batch_lens[i];
+    if (threadIdx.x == 0) {
+      at = atomicAdd(cursor, (unsigned long long)((len + 15u) & ~15u));
+      pack_offs[i] = at;
+    }
+    __syncthreads();
+    const uint4 *src = reinterpret_cast<const uint4 *>(d_out + out_offs[i]);  // 256-aligned
+    uint4 *dst = reinterpret_cast<uint4 *>(h_out + at);                        // 16-aligned
+    for (uint32_t v = threadIdx.x; v < (len + 15u) / 16u; v += blockDim.x) dst[v] = src[v];
+    __syncthreads();
+  }
+}
 
 int launch(rdk_hip_producer_s *p, Slot &sl) {
   const uint32_t B = p->max_batches, n = sl.nb;
@@ -148,7 +177,12 @@ int launch(rdk_hip_producer_s *p, Slot &sl) {
   if ((rc = rdk_hip_msgset_v2_crc(sl.d_out, dm.out_offs, dm.caps, dm.crcs, n,
                                   RDK_HIP_V2_CRC_FINALIZE, sl.s)))
     return rc;
-  RDK_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sl.out_used, hipMemcpyDeviceToHost, sl.s));
+  RDK_HIP_CHECK(hipMemsetAsync(dm.cursor, 0, 8, sl.s));
+  hipLaunchKernelGGL(pack_to_host_kernel, dim3(n < 2048u ? n : 2048u), dim3(256), 0, sl.s,
+                     sl.d_out, dm.out_offs, dm.batch_lens, n, sl.dh_out, dm.pack_offs,
+                     dm.cursor);
+  RDK_HIP_CHECK(hipGetLastError());
+  RDK_HIP_CHECK(hipMemcpyAsync(hm.pack_offs, dm.pack_offs, size_t(n) * 8, hipMemcpyDeviceToHost, sl.s));
   RDK_HIP_CHECK(hipMemcpyAsync(hm.batch_lens, dm.batch_lens, size_t(n) * 4, hipMemcpyDeviceToHost, sl.s));
   RDK_HIP_CHECK(hipMemcpyAsync(hm.crcs, dm.crcs, size_t(n) * 4, hipMemcpyDeviceToHost, sl.s));
   RDK_HIP_CHECK(hipEventRecord(sl.done, sl.s));
@@ -194,7 +228,9 @@ RDK_API rdk_hip_producer_t *rdk_hip_producer_new(int device, size_t slot_bytes, 
     if (hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&sl.h_in), slot_bytes, 0) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&sl.h_out), p->out_bytes, 0) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&sl.h_out), p->out_bytes,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&sl.dh_out), sl.h_out, 0) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&sl.h_meta), mb, 0) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&sl.d_in), slot_bytes + 256) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&sl.d_out), p->out_bytes) != hipSuccess ||
@@ -270,7 +306,7 @@ RDK_API int rdk_hip_producer_poll(rdk_hip_producer_t *p, rdk_hip_batch_t *out, i
     Meta hm = meta_at(sl.h_meta, p->max_batches);
     while (got < max && sl.polled < sl.nb) {
       const uint32_t i = sl.polled++;
-      out[got].data = sl.h_out + hm.out_offs[i];
+      out[got].data = sl.h_out + hm.pack_offs[i];
       out[got].len = hm.batch_lens[i];
       out[got].crc = hm.crcs[i];
       out[got].cookie = sl.cookies[i];

@@ -117,3 +117,12 @@ def test_v2_index_big_records_and_errors(engine, oracle_mod):
     for i in range(4):
         _check_index(oracle_mod, bs[i], cnt[i], host, r0[i])
     assert cnt[4] == -(1 + 10)                          # row capacity 10: record 10 fails
+
+
+def test_v2_index_large_batches(engine, oracle_mod):
+    """~1 MiB batches (many LDS windows, records ending exactly at window edges)."""
+    m = W.gen_messages(19000, seed=21)
+    bs = [oracle_mod.msgset_v2_write(m, 0, 9500), oracle_mod.msgset_v2_write(m, 9500, 9500)]
+    cnt, host, r0 = _index(engine, bs)
+    for i, b in enumerate(bs):
+        _check_index(oracle_mod, b, cnt[i], host, r0[i])

@@ -59,6 +59,12 @@ void crc32c_global_init(void);
  * rd_slice_reader() loop it replaces. */
 uint32_t rd_slice_crc32c(rd_slice_t *slice);
 
+/* Replaces rd_slice_crc32() (src/rdbuf.c:1093-1104): CRC-32 (zlib crc32(),
+ * rdcrc32.h:93-131 under WITH_ZLIB) of the slice's remaining segments, leaving
+ * the slice consumed.  The MsgVersion 0/1 reader's check.crcs site
+ * (rdkafka_msgset_reader.c:606). */
+uint32_t rd_slice_crc32(rd_slice_t *slice);
+
 /* Replaces rd_kafka_lz4_compress() (src/rdkafka_lz4.c:329-442).  LZ4F frame
  * with prefs {blockIndependent, comp_level}, 64 KB blocks; *outbuf is
  * malloc()ed (caller frees with free()); slice is consumed.  comp_level >= 3
@@ -98,6 +104,32 @@ const char *rdk_hip_version(void);
 int rdk_hip_crc32c_ranges(const void *d_base, const uint64_t *d_offs,
                           const uint32_t *d_lens, const uint32_t *d_init,
                           uint32_t *d_out, uint32_t n, void *stream);
+
+/* Same for CRC-32 (zlib crc32(): MsgVersion 0/1, rdcrc32.h:93-131). */
+int rdk_hip_crc32_ranges(const void *d_base, const uint64_t *d_offs,
+                         const uint32_t *d_lens, const uint32_t *d_init,
+                         uint32_t *d_out, uint32_t n, void *stream);
+
+/* MsgVersion 0/1 MessageSets at d_base + d_set_offs[i], d_set_lens[i] bytes:
+ * the reader's message walk and check.crcs (rd_kafka_msgset_reader_msg_v0_1,
+ * rdkafka_msgset_reader.c:538-628) / the writer's per-message Crc
+ * (rd_kafka_msgset_writer_write_msg_v0_1, rdkafka_msgset_writer.c:583-645).
+ * Message k of set i goes to row d_row_offs[i] + k (at most d_row_caps[i]):
+ *   d_msg_pos[row] = message start (its Offset field) from the set start
+ *   d_msg_out[row] = CRC-32 of [16, 12+MessageSize) (mode COMPUTE / FINALIZE,
+ *                    FINALIZE also stores it big-endian at the Crc field, +12)
+ *                    or 0 / 1 = stored Crc matches / does not (mode VERIFY; the
+ *                    reader skips such a message and continues, :612-627)
+ *   d_count[i]     = number of whole messages (a partial message at the end
+ *                    stops the walk, :599-600), or -(1+k) when message k fails
+ *                    the header checks (MessageSize < hdrsize :590-597, or < 4)
+ *                    or does not fit in the rows.
+ * Modes are RDK_HIP_V2_CRC_COMPUTE / _FINALIZE / _VERIFY. */
+int rdk_hip_msgset_v01_crc(void *d_base, const uint64_t *d_set_offs,
+                           const uint32_t *d_set_lens, const uint64_t *d_row_offs,
+                           const uint32_t *d_row_caps, uint32_t *d_msg_pos,
+                           uint32_t *d_msg_out, int32_t *d_count, uint32_t n, int mode,
+                           void *stream);
 
 /* MsgVersion 2 record batches laid out at d_base + d_batch_offs[i].  The CRC
  * range is [21, 12+Length) read from each header (big-endian Length at 8),

@@ -50,7 +50,8 @@ EXPORTED_SYMBOLS = (
     "rdk_hip_gen_v2_batches", "rdk_hip_producer_new", "rdk_hip_producer_produce",
     "rdk_hip_producer_flush", "rdk_hip_producer_poll", "rdk_hip_producer_destroy",
     "rdk_hip_gen_json", "rdk_hip_msgset_v2_sizes", "rdk_hip_msgset_v2_write",
-    "rdk_hip_msgset_v2_index",
+    "rdk_hip_msgset_v2_index", "rd_slice_crc32", "rdk_hip_crc32_ranges",
+    "rdk_hip_msgset_v01_crc",
 )
 
 
@@ -81,6 +82,8 @@ def lib():
     L.crc32c_global_init.restype = None
     L.rd_slice_crc32c.restype = u32
     L.rd_slice_crc32c.argtypes = [vp]
+    L.rd_slice_crc32.restype = u32
+    L.rd_slice_crc32.argtypes = [vp]
     L.rd_kafka_lz4_compress.restype = i32
     L.rd_kafka_lz4_compress.argtypes = [vp, i32, i32, vp, C.POINTER(vp), C.POINTER(sz)]
     L.rd_kafka_lz4_decompress.restype = i32
@@ -91,6 +94,10 @@ def lib():
     L.rdk_hip_version.restype = C.c_char_p
     L.rdk_hip_crc32c_ranges.restype = i32
     L.rdk_hip_crc32c_ranges.argtypes = [vp, vp, vp, vp, vp, u32, vp]
+    L.rdk_hip_crc32_ranges.restype = i32
+    L.rdk_hip_crc32_ranges.argtypes = [vp, vp, vp, vp, vp, u32, vp]
+    L.rdk_hip_msgset_v01_crc.restype = i32
+    L.rdk_hip_msgset_v01_crc.argtypes = [vp] * 8 + [u32, i32, vp]
     L.rdk_hip_msgset_v2_crc.restype = i32
     L.rdk_hip_msgset_v2_crc.argtypes = [vp, vp, vp, vp, u32, i32, vp]
     if hasattr(L, "rdk_hip_lz4f_compress"):
@@ -238,6 +245,12 @@ def rd_slice_crc32c(slice_or_segments) -> int:
     return lib().rd_slice_crc32c(s.ptr)
 
 
+def rd_slice_crc32(slice_or_segments) -> int:
+    """rd_slice_crc32() (src/rdbuf.c:1093, zlib CRC-32) on the GPU; consumes the slice."""
+    s = slice_or_segments if isinstance(slice_or_segments, RdSlice) else RdSlice(slice_or_segments)
+    return lib().rd_slice_crc32(s.ptr)
+
+
 def rd_kafka_lz4_compress(proper_hc: int, comp_level: int, slice_or_segments) -> tuple[int, bytes]:
     """rd_kafka_lz4_compress() (src/rdkafka_lz4.c:329): (err, frame)."""
     s = slice_or_segments if isinstance(slice_or_segments, RdSlice) else RdSlice(
@@ -300,6 +313,23 @@ def crc32c_ranges(base, offs, lens, out, init=None, stream=None) -> None:
     """CRC32C of device ranges base[offs[i]:offs[i]+lens[i]] -> out[i] (uint32)."""
     _check(lib().rdk_hip_crc32c_ranges(_ptr(base), _ptr(offs), _ptr(lens), _ptr(init), _ptr(out),
                                        int(offs.numel()), _stream(stream)), "crc32c_ranges")
+
+
+def crc32_ranges(base, offs, lens, out, init=None, stream=None) -> None:
+    """CRC-32 (zlib crc32(), MsgVersion 0/1) of device ranges -> out[i] (uint32)."""
+    _check(lib().rdk_hip_crc32_ranges(_ptr(base), _ptr(offs), _ptr(lens), _ptr(init), _ptr(out),
+                                      int(offs.numel()), _stream(stream)), "crc32_ranges")
+
+
+def msgset_v01_crc(base, set_offs, set_lens, row_offs, row_caps, msg_pos, msg_out, count,
+                   mode=V2_CRC_COMPUTE, stream=None) -> None:
+    """MsgVersion 0/1 MessageSets on device: per-message CRC-32 compute / finalize / verify
+    (rdkafka_msgset_reader.c:538-628, rdkafka_msgset_writer.c:583-645); see
+    include/librdkafka_hip.h for the row / count layout."""
+    _check(lib().rdk_hip_msgset_v01_crc(_ptr(base), _ptr(set_offs), _ptr(set_lens),
+                                        _ptr(row_offs), _ptr(row_caps), _ptr(msg_pos),
+                                        _ptr(msg_out), _ptr(count), int(set_offs.numel()), mode,
+                                        _stream(stream)), "msgset_v01_crc")
 
 
 def msgset_v2_crc(base, batch_offs, batch_caps, out, mode=V2_CRC_COMPUTE, stream=None) -> None:

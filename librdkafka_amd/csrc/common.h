@@ -41,12 +41,14 @@ int ensure_host(Ctx *c, size_t bytes);
 int ensure_dev(Ctx *c, int which, size_t bytes);
 int ensure_desc(Ctx *c, size_t bytes);
 
-// Device-resident CRC tables for `device` (uploaded once per device).
-const uint32_t *crc_tables_dev(int device);     // v1: byte slicing-by-16 image
-const uint32_t *crc_tables_v3_dev(int device);  // v3: rotated-nibble image
+// Device-resident CRC tables for `device` (uploaded once per device).  kind selects the
+// polynomial: kCrcKind32C (CRC-32C, crc32c.c) or kCrcKind32 (CRC-32/zlib, rdcrc32.h).
+constexpr int kCrcKind32C = 0, kCrcKind32 = 1;
+const uint32_t *crc_tables_dev(int device, int kind = kCrcKind32C);     // v1: slicing-by-16 image
+const uint32_t *crc_tables_v3_dev(int device, int kind = kCrcKind32C);  // v3: rotated-nibble image
+const uint32_t *crc_tables_v4_dev(int device, int kind = kCrcKind32C);  // v4: 16-lane-group image
 // x^(2^k) mod P table (k = 0..63) for arbitrary-length shifts.
-const uint32_t *crc_tables_v4_dev(int device);  // v4: 16-lane-group byte-table image
-const uint32_t *crc_x2n_dev(int device);
+const uint32_t *crc_x2n_dev(int device, int kind = kCrcKind32C);
 
 // Aborts the process with a message (drop-in symbols have no error channel).
 [[noreturn]] void fatal(const char *what);

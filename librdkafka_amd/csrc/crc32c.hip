@@ -570,34 +570,34 @@ __global__ __launch_bounds__(crc_block<V>(), 8) void crc32c_chunks_kernel(
 }
 
 // multiply in GF(2)[x]/P, reflected (bit 31 = x^0)
-__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b, uint32_t poly) {
   uint32_t m = 1u << 31, p = 0;
   for (int i = 0; i < 32; ++i) {
     if (a & m) p ^= b;
     m >>= 1;
-    b = (b & 1u) ? (b >> 1) ^ kCrcPoly : b >> 1;
+    b = (b & 1u) ? (b >> 1) ^ poly : b >> 1;
   }
   return p;
 }
 
 // register advanced by `nbytes` zero bytes
-__device__ uint32_t shift_bytes(uint32_t x, uint64_t nbytes, const uint32_t *x2n) {
+__device__ uint32_t shift_bytes(uint32_t x, uint64_t nbytes, const uint32_t *x2n, uint32_t poly) {
   uint32_t p = 1u << 31;
   int k = 3;
   for (uint64_t n = nbytes; n; n >>= 1, ++k)
-    if (n & 1u) p = multmodp(x2n[k], p);
-  return multmodp(p, x);
+    if (n & 1u) p = multmodp(x2n[k], p, poly);
+  return multmodp(p, x, poly);
 }
 
 __global__ void crc32c_combine_kernel(const uint32_t *__restrict__ raw, uint32_t nchunks,
                                       uint64_t len, uint32_t *__restrict__ out,
-                                      const uint32_t *__restrict__ x2n) {
+                                      const uint32_t *__restrict__ x2n, uint32_t poly) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint32_t x = raw[0];
   for (uint32_t i = 1; i < nchunks; ++i) {
     const uint64_t o = uint64_t(i) * kCrcChunk;
     const uint64_t l = (len - o < kCrcChunk) ? len - o : kCrcChunk;
-    x = shift_bytes(x, l, x2n) ^ raw[i];
+    x = shift_bytes(x, l, x2n, poly) ^ raw[i];
   }
   *out = ~x;
 }
@@ -777,7 +777,7 @@ __device__ uint32_t xpow8n(uint64_t nbytes, const uint32_t *x2n) {  // x^(8*nbyt
   uint32_t p = 1u << 31;
   int k = 3;
   for (uint64_t n = nbytes; n; n >>= 1, ++k)
-    if (n & 1u) p = multmodp(x2n[k], p);
+    if (n & 1u) p = multmodp(x2n[k], p, kCrcPoly);
   return p;
 }
 
@@ -803,7 +803,7 @@ __global__ void crc32c_msgset_v2_combine_kernel(uint8_t *__restrict__ base,
   uint32_t r = raw[size_t(i) * nch];
   for (uint32_t j = 1; j < nch && uint64_t(j) * C < len; ++j) {
     const uint32_t cl = (uint64_t(j + 1) * C <= len) ? C : len - j * C;
-    r = multmodp(cl == C ? pc : xpow8n(cl, x2n), r) ^ raw[size_t(i) * nch + j];
+    r = multmodp(cl == C ? pc : xpow8n(cl, x2n), r, kCrcPoly) ^ raw[size_t(i) * nch + j];
   }
   const uint32_t crc = ~r;
   if (MODE == RDK_HIP_V2_CRC_VERIFY) {
@@ -849,32 +849,34 @@ template <int V> static unsigned crc_grid(uint32_t nwork) {
   return blocks ? blocks : 1u;
 }
 
-template <int V> static const uint32_t *tabs(int dev) {
-  return V == 3 ? crc_tables_v3_dev(dev) : crc_tables_dev(dev);
+template <int V> static const uint32_t *tabs(int dev, int kind = kCrcKind32C) {
+  return V == 3 ? crc_tables_v3_dev(dev, kind) : crc_tables_dev(dev, kind);
 }
 template <int V> static size_t lds_bytes() { return size_t(crc_lds_words<V>()) * 4u; }
 
 template <int V>
 static void launch_chunks(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
-                          uint32_t *d_scratch, uint32_t nchunks, hipStream_t s) {
+                          uint32_t *d_scratch, uint32_t nchunks, hipStream_t s, int kind) {
   hipLaunchKernelGGL(crc32c_chunks_kernel<V>, dim3(crc_grid<V>(nchunks)), dim3(crc_block<V>()),
-                     lds_bytes<V>(), s, d_buf, len, init, d_scratch, nchunks, tabs<V>(c->device));
+                     lds_bytes<V>(), s, d_buf, len, init, d_scratch, nchunks,
+                     tabs<V>(c->device, kind));
 }
 
 // CRC32C of one device buffer (any length) -> d_scratch[nchunks] (device).
 // Used by the drop-in crc32c()/rd_slice_crc32c() after the host gather + H2D.
 int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
-                      uint32_t *d_scratch /* >= nchunks+1 words */, hipStream_t s) {
+                      uint32_t *d_scratch /* >= nchunks+1 words */, hipStream_t s, int kind) {
   const uint32_t nchunks = len ? uint32_t((len + kCrcChunk - 1) / kCrcChunk) : 1u;
   if (len == 0) {
     // crc32c(crc, buf, 0) == crc: inversions cancel (crc32c.c:102,133)
     RDK_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_scratch + nchunks), init, 1, s));
     return 0;
   }
-  if (crc_variant() != 1) launch_chunks<3>(c, d_buf, len, init, d_scratch, nchunks, s);
-  else launch_chunks<1>(c, d_buf, len, init, d_scratch, nchunks, s);
+  if (crc_variant() != 1) launch_chunks<3>(c, d_buf, len, init, d_scratch, nchunks, s, kind);
+  else launch_chunks<1>(c, d_buf, len, init, d_scratch, nchunks, s, kind);
   hipLaunchKernelGGL(crc32c_combine_kernel, dim3(1), dim3(64), 0, s, d_scratch, nchunks, len,
-                     d_scratch + nchunks, crc_x2n_dev(c->device));
+                     d_scratch + nchunks, crc_x2n_dev(c->device, kind),
+                     kind == kCrcKind32 ? kCrc32Poly : kCrcPoly);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -886,10 +888,31 @@ uint32_t crc_scratch_words(uint64_t len) {
 template <int V>
 static void launch_ranges(Ctx *c, const void *d_base, const uint64_t *d_offs,
                           const uint32_t *d_lens, const uint32_t *d_init, uint32_t *d_out,
-                          uint32_t n, hipStream_t s) {
+                          uint32_t n, hipStream_t s, int kind) {
   hipLaunchKernelGGL(crc32c_ranges_kernel<V>, dim3(crc_grid<V>(n)), dim3(crc_block<V>()),
                      lds_bytes<V>(), s, static_cast<const uint8_t *>(d_base), d_offs, d_lens,
-                     d_init, d_out, n, tabs<V>(c->device));
+                     d_init, d_out, n, tabs<V>(c->device, kind));
+}
+
+// n ranges of either polynomial (the kernels are polynomial-agnostic: they take the image)
+static int ranges_any(const void *d_base, const uint64_t *d_offs, const uint32_t *d_lens,
+                      const uint32_t *d_init, uint32_t *d_out, uint32_t n, void *stream,
+                      int kind) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_base || !d_offs || !d_lens || !d_out) return set_error(RDK_HIP_E_INVAL, "null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (crc_variant() == 4)
+    hipLaunchKernelGGL(crc32c_ranges_v4_kernel, dim3(crc_grid_v4(n)), dim3(kV4Block), 0, s,
+                       static_cast<const uint8_t *>(d_base), d_offs, d_lens, d_init, d_out, n,
+                       crc_tables_v4_dev(c->device, kind));
+  else if (crc_variant() == 3)
+    launch_ranges<3>(c, d_base, d_offs, d_lens, d_init, d_out, n, s, kind);
+  else
+    launch_ranges<1>(c, d_base, d_offs, d_lens, d_init, d_out, n, s, kind);
+  RDK_HIP_CHECK(hipGetLastError());
+  return RDK_HIP_OK;
 }
 
 template <int V, int MODE>
@@ -932,19 +955,13 @@ using namespace rdk;
 RDK_API int rdk_hip_crc32c_ranges(const void *d_base, const uint64_t *d_offs,
                                   const uint32_t *d_lens, const uint32_t *d_init,
                                   uint32_t *d_out, uint32_t n, void *stream) {
-  Ctx *c = ctx();
-  if (!c) return RDK_HIP_E_NODEV;
-  if (!n) return RDK_HIP_OK;
-  if (!d_base || !d_offs || !d_lens || !d_out) return set_error(RDK_HIP_E_INVAL, "null pointer");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (crc_variant() == 4)
-    hipLaunchKernelGGL(crc32c_ranges_v4_kernel, dim3(crc_grid_v4(n)), dim3(kV4Block), 0, s,
-                       static_cast<const uint8_t *>(d_base), d_offs, d_lens, d_init, d_out, n,
-                       crc_tables_v4_dev(c->device));
-  else if (crc_variant() == 3) launch_ranges<3>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
-  else launch_ranges<1>(c, d_base, d_offs, d_lens, d_init, d_out, n, s);
-  RDK_HIP_CHECK(hipGetLastError());
-  return RDK_HIP_OK;
+  return ranges_any(d_base, d_offs, d_lens, d_init, d_out, n, stream, kCrcKind32C);
+}
+
+RDK_API int rdk_hip_crc32_ranges(const void *d_base, const uint64_t *d_offs,
+                                 const uint32_t *d_lens, const uint32_t *d_init,
+                                 uint32_t *d_out, uint32_t n, void *stream) {
+  return ranges_any(d_base, d_offs, d_lens, d_init, d_out, n, stream, kCrcKind32);
 }
 
 RDK_API int rdk_hip_msgset_v2_crc(void *d_base, const uint64_t *d_batch_offs,

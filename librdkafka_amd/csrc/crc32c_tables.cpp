@@ -22,9 +22,9 @@ static void gf2_compose(uint32_t dst[32], const uint32_t a[32], const uint32_t b
 // Operator appending `nbytes` zero bytes to a raw (un-inverted) CRC register.
 // Column i = image of register bit i.  One zero BIT maps bit 0 -> poly and
 // bit i -> bit i-1 (reflected shift), as in crc32c_zeros_op (crc32c.c:173).
-void crc_zeros_operator(uint32_t op[32], size_t nbytes) {
+void crc_zeros_operator(uint32_t op[32], size_t nbytes, uint32_t poly) {
   uint32_t p[32];
-  p[0] = kCrcPoly;
+  p[0] = poly;
   for (int i = 1; i < 32; ++i) p[i] = 1u << (i - 1);
   for (int k = 0; k < 3; ++k) gf2_compose(p, p, p);  // 1 bit -> 8 bits
   for (int i = 0; i < 32; ++i) op[i] = 1u << i;        // identity
@@ -35,12 +35,12 @@ void crc_zeros_operator(uint32_t op[32], size_t nbytes) {
   }
 }
 
-void crc_build_tables(uint32_t *out) {
+void crc_build_tables(uint32_t *out, uint32_t poly) {
   // byte-wise table, then slicing extension (crc32c.c:69-92 generalised to 16)
   uint32_t *T = out;
   for (uint32_t b = 0; b < 256; ++b) {
     uint32_t r = b;
-    for (int i = 0; i < 8; ++i) r = (r >> 1) ^ ((r & 1u) ? kCrcPoly : 0u);
+    for (int i = 0; i < 8; ++i) r = (r >> 1) ^ ((r & 1u) ? poly : 0u);
     T[b] = r;
   }
   for (int k = 1; k < kCrcSliceTables; ++k)
@@ -51,18 +51,18 @@ void crc_build_tables(uint32_t *out) {
   // shift operators for 32..1024 bytes, split per state byte
   for (int level = 1; level <= 6; ++level) {
     uint32_t op[32];
-    crc_zeros_operator(op, size_t(16) << level);
+    crc_zeros_operator(op, size_t(16) << level, poly);
     uint32_t *S = out + crc_shift_table(level) * 256;
     for (int j = 0; j < 4; ++j)
       for (uint32_t b = 0; b < 256; ++b) S[j * 256 + b] = crc_gf2_times(op, b << (8 * j));
   }
 }
 
-void crc_build_tables_v3(uint32_t *out) {
+void crc_build_tables_v3(uint32_t *out, uint32_t poly) {
   std::memset(out, 0, size_t(kCrcV3Bytes));
   uint32_t op[32];
   for (int map = 0; map < 2; ++map) {
-    crc_zeros_operator(op, map == 0 ? size_t(kLaneStride - 12) : size_t(4));
+    crc_zeros_operator(op, map == 0 ? size_t(kLaneStride - 12) : size_t(4), poly);
     for (int j = 0; j < 4; ++j)      // rotation y_j = rotr(x, 8j)
       for (int h = 0; h < 2; ++h)    // group at bits 7+4h .. 10+4h of y_j
         for (uint32_t e = 0; e < 16; ++e) {
@@ -78,22 +78,22 @@ void crc_build_tables_v3(uint32_t *out) {
         }
   }
   for (int m = 0; m < 6; ++m) {  // merge tree: advance by 16 << m bytes
-    crc_zeros_operator(op, size_t(16) << m);
+    crc_zeros_operator(op, size_t(16) << m, poly);
     for (int q = 0; q < 4; ++q)
       for (uint32_t b = 0; b < 256; ++b)
         out[v3_byte_table(m * 4 + q) / 4 + int(b)] = crc_gf2_times(op, b << (8 * q));
   }
   for (uint32_t b = 0; b < 256; ++b) {  // T0 (crc32c.c:69-78)
     uint32_t r = b;
-    for (int i = 0; i < 8; ++i) r = (r >> 1) ^ ((r & 1u) ? kCrcPoly : 0u);
+    for (int i = 0; i < 8; ++i) r = (r >> 1) ^ ((r & 1u) ? poly : 0u);
     out[v3_byte_table(kV3T0) / 4 + int(b)] = r;
   }
 }
 
-void crc_build_tables_v4(uint32_t *out) {
+void crc_build_tables_v4(uint32_t *out, uint32_t poly) {
   std::memset(out, 0, size_t(kCrcV4Bytes));
   uint32_t op[32];
-  crc_zeros_operator(op, size_t(kV4Step));
+  crc_zeros_operator(op, size_t(kV4Step), poly);
   for (int q = 0; q < 4; ++q)
     for (uint32_t b = 0; b < 256; ++b) {
       const uint32_t v = crc_gf2_times(op, b << (8 * q));
@@ -101,18 +101,18 @@ void crc_build_tables_v4(uint32_t *out) {
         out[((q >> 1) * 0x10000 + int(b) * 256 + (q & 1) * 128 + c * 4) / 4] = v;
     }
   for (int l = 0; l < kV4Lanes; ++l) {  // Fin: group lane l's last dword stream ends
-    crc_zeros_operator(op, size_t(kV4Row - 16 * l - 12));  // kV4Row-16l-12 bytes early
+    crc_zeros_operator(op, size_t(kV4Row - 16 * l - 12), poly);  // kV4Row-16l-12 bytes early
     for (int i = 0; i < 8; ++i)
       for (uint32_t n = 0; n < 16; ++n) {
         const uint32_t v = crc_gf2_times(op, n << (4 * i));
         for (int c = l; c < 32; c += kV4Lanes) out[(kV4Fin + i * 2048 + int(n) * 128 + c * 4) / 4] = v;
       }
   }
-  crc_zeros_operator(op, 4);
+  crc_zeros_operator(op, 4, poly);
   for (int q = 0; q < 4; ++q)
     for (uint32_t b = 0; b < 256; ++b)
       out[(kV4Z4 + q * 1024) / 4 + int(b)] = crc_gf2_times(op, b << (8 * q));
-  crc_zeros_operator(op, size_t(kV4Row));
+  crc_zeros_operator(op, size_t(kV4Row), poly);
   for (int q = 0; q < 4; ++q)
     for (uint32_t b = 0; b < 256; ++b)
       out[(kV4Z256 + q * 1024) / 4 + int(b)] = crc_gf2_times(op, b << (8 * q));
@@ -120,7 +120,7 @@ void crc_build_tables_v4(uint32_t *out) {
 
 // x2n[k] = x^(2^k) mod P in reflected form (bit 31 = x^0), for the
 // multiply-mod-P shift used when combining ranges of arbitrary length.
-static uint32_t multmodp(uint32_t a, uint32_t b) {
+static uint32_t multmodp(uint32_t a, uint32_t b, uint32_t poly) {
   uint32_t m = 1u << 31, p = 0;
   for (;;) {
     if (a & m) {
@@ -128,15 +128,15 @@ static uint32_t multmodp(uint32_t a, uint32_t b) {
       if ((a & (m - 1)) == 0) break;
     }
     m >>= 1;
-    b = (b & 1u) ? (b >> 1) ^ kCrcPoly : b >> 1;
+    b = (b & 1u) ? (b >> 1) ^ poly : b >> 1;
   }
   return p;
 }
 
-void crc_build_x2n(uint32_t *out) {
+void crc_build_x2n(uint32_t *out, uint32_t poly) {
   uint32_t p = 1u << 30;  // x^1
   out[0] = p;
-  for (int k = 1; k < 64; ++k) out[k] = p = multmodp(p, p);
+  for (int k = 1; k < 64; ++k) out[k] = p = multmodp(p, p, poly);
 }
 
 }  // namespace rdk

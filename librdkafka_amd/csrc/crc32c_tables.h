@@ -15,6 +15,10 @@
 namespace rdk {
 
 constexpr uint32_t kCrcPoly = 0x82f63b78u;
+// CRC-32 (IEEE 802.3, zlib crc32()): MsgVersion 0/1 messages (rdcrc32.h:93-131 with
+// WITH_ZLIB).  Same reflected register, init and final inversion, other polynomial: every
+// image below is built for either polynomial and the kernels take the image they are given.
+constexpr uint32_t kCrc32Poly = 0xedb88320u;
 
 // LDS image layout (40 tables x 256 u32 = 40 KiB):
 //   tables 0..15   : T[k][b] = raw CRC of byte b followed by k zero bytes
@@ -27,7 +31,7 @@ constexpr int kCrcTableWords = kCrcNumTables * 256;
 // index of the first of the 4 tables for shift-by-(16 << level), level 1..6
 constexpr int crc_shift_table(int level) { return kCrcShiftBase + 4 * (level - 1); }
 
-void crc_build_tables(uint32_t *out /* kCrcTableWords */);
+void crc_build_tables(uint32_t *out /* kCrcTableWords */, uint32_t poly = kCrcPoly);
 
 // ---- v3 image (default): rotated-nibble tables, conflict-free and 1-VALU addresses
 // A 32->32 GF(2)-linear map F (the CRC register advanced over n zero bytes) is
@@ -53,8 +57,8 @@ constexpr int kCrcV3Words = kCrcV3Bytes / 4;
 constexpr int kLaneStride = 1024;               // bytes between a lane's vectors
 // byte offset of byte table i (256 dwords, contiguous)
 constexpr int v3_byte_table(int i) { return i < 16 ? i * 2048 + 1024 : kV3ByteHi + (i - 16) * 1024; }
-void crc_build_tables_v3(uint32_t *out /* kCrcV3Words */);
-void crc_build_x2n(uint32_t *out /* 64 */);
+void crc_build_tables_v3(uint32_t *out /* kCrcV3Words */, uint32_t poly = kCrcPoly);
+void crc_build_x2n(uint32_t *out /* 64 */, uint32_t poly = kCrcPoly);
 
 // ---- v4 image (batched ranges / MsgVersion 2 kernels): 16-lane groups, byte tables
 // A 16-lane group CRCs one range.  Per step the group reads kV4Vecs x 256 contiguous bytes:
@@ -87,10 +91,10 @@ constexpr int kV4T0 = kV4Z4 + 3 * 1024;
 constexpr int kV4Z256 = 0x25000;                // Z_kV4Row: byte table q at +1024*q
 constexpr int kCrcV4Bytes = kV4Z256 + 4 * 1024; // 155648 B = 152 KiB (one workgroup per CU)
 constexpr int kCrcV4Words = kCrcV4Bytes / 4;
-void crc_build_tables_v4(uint32_t *out /* kCrcV4Words */);
+void crc_build_tables_v4(uint32_t *out /* kCrcV4Words */, uint32_t poly = kCrcPoly);
 
 // Host GF(2) helpers (also used by unit tests through the engine API).
 uint32_t crc_gf2_times(const uint32_t mat[32], uint32_t vec);
-void crc_zeros_operator(uint32_t op[32], size_t nbytes);
+void crc_zeros_operator(uint32_t op[32], size_t nbytes, uint32_t poly = kCrcPoly);
 
 }  // namespace rdk

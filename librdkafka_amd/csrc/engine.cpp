@@ -40,40 +40,44 @@ const char *last_error() { return tl_err; }
 namespace {
 constexpr int kMaxDev = 64;
 std::mutex g_mu;
-uint32_t *g_tables[kMaxDev];
-uint32_t *g_tables_v3[kMaxDev];
-uint32_t *g_tables_v4[kMaxDev];
-uint32_t *g_x2n[kMaxDev];
+// [kind][device]: kind 0 = CRC-32C (MsgVersion 2), 1 = CRC-32 (MsgVersion 0/1)
+uint32_t *g_tables[2][kMaxDev];
+uint32_t *g_tables_v3[2][kMaxDev];
+uint32_t *g_tables_v4[2][kMaxDev];
+uint32_t *g_x2n[2][kMaxDev];
 
 int default_device() {
   const char *e = getenv("RDK_HIP_DEVICE");
   return e ? atoi(e) : 0;
 }
 
+template <size_t N>
+int upload(uint32_t **dst, const uint32_t (&host)[N]) {
+  RDK_HIP_CHECK(hipMalloc(dst, sizeof host));
+  RDK_HIP_CHECK(hipMemcpy(*dst, host, sizeof host, hipMemcpyHostToDevice));
+  return 0;
+}
+
 int upload_tables(int dev) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_tables[dev]) return 0;
+  if (g_tables[1][dev]) return 0;
   static uint32_t host_tab[kCrcTableWords];
   static uint32_t host_tab2[kCrcV3Words];
   static uint32_t host_tab4[kCrcV4Words];
   static uint32_t host_x2n[64];
-  crc_build_tables(host_tab);
-  crc_build_tables_v4(host_tab4);
-  crc_build_tables_v3(host_tab2);
-  crc_build_x2n(host_x2n);
-  uint32_t *d = nullptr, *d2 = nullptr, *d4 = nullptr, *x = nullptr;
-  RDK_HIP_CHECK(hipMalloc(&d4, sizeof host_tab4));
-  RDK_HIP_CHECK(hipMemcpy(d4, host_tab4, sizeof host_tab4, hipMemcpyHostToDevice));
-  RDK_HIP_CHECK(hipMalloc(&d, sizeof host_tab));
-  RDK_HIP_CHECK(hipMalloc(&d2, sizeof host_tab2));
-  RDK_HIP_CHECK(hipMalloc(&x, sizeof host_x2n));
-  RDK_HIP_CHECK(hipMemcpy(d, host_tab, sizeof host_tab, hipMemcpyHostToDevice));
-  RDK_HIP_CHECK(hipMemcpy(d2, host_tab2, sizeof host_tab2, hipMemcpyHostToDevice));
-  RDK_HIP_CHECK(hipMemcpy(x, host_x2n, sizeof host_x2n, hipMemcpyHostToDevice));
-  g_tables[dev] = d;
-  g_tables_v3[dev] = d2;
-  g_tables_v4[dev] = d4;
-  g_x2n[dev] = x;
+  for (int kind = 0; kind < 2; ++kind) {
+    const uint32_t poly = kind ? kCrc32Poly : kCrcPoly;
+    crc_build_tables(host_tab, poly);
+    crc_build_tables_v4(host_tab4, poly);
+    crc_build_tables_v3(host_tab2, poly);
+    crc_build_x2n(host_x2n, poly);
+    int rc;
+    if ((rc = upload(&g_tables_v4[kind][dev], host_tab4)) ||
+        (rc = upload(&g_tables[kind][dev], host_tab)) ||
+        (rc = upload(&g_tables_v3[kind][dev], host_tab2)) ||
+        (rc = upload(&g_x2n[kind][dev], host_x2n)))
+      return rc;
+  }
   return 0;
 }
 
@@ -166,10 +170,10 @@ int ensure_desc(Ctx *c, size_t bytes) {
   return 0;
 }
 
-const uint32_t *crc_tables_dev(int device) { return g_tables[device]; }
-const uint32_t *crc_tables_v3_dev(int device) { return g_tables_v3[device]; }
-const uint32_t *crc_tables_v4_dev(int device) { return g_tables_v4[device]; }
-const uint32_t *crc_x2n_dev(int device) { return g_x2n[device]; }
+const uint32_t *crc_tables_dev(int device, int kind) { return g_tables[kind][device]; }
+const uint32_t *crc_tables_v3_dev(int device, int kind) { return g_tables_v3[kind][device]; }
+const uint32_t *crc_tables_v4_dev(int device, int kind) { return g_tables_v4[kind][device]; }
+const uint32_t *crc_x2n_dev(int device, int kind) { return g_x2n[kind][device]; }
 
 }  // namespace rdk
 

@@ -1,0 +1,392 @@
+// legacy.hip -- MsgVersion 0/1 MessageSets: the per-message CRC-32.
+//
+// Reference (bluelichen19/librdkafka v1.3.0):
+//   writer  rd_kafka_msgset_writer_write_msg_v0_1  src/rdkafka_msgset_writer.c:583-645
+//           (Offset, MessageSize, Crc = CRC-32 over MagicByte..Value, :613-641)
+//   reader  rd_kafka_msgset_reader_msg_v0_1        src/rdkafka_msgset_reader.c:538-640
+//           (header reads :566-587, MessageSize < hdrsize :590-597, partial :599-600,
+//           check.crcs :602-628 through rd_slice_crc32, rdbuf.c:1093-1104)
+//   CRC-32  rdcrc32.h:93-131 with WITH_ZLIB: zlib crc32(), reflected 0xedb88320
+//
+// A MessageSet is a chain: message p is [p, p + 12 + MessageSize) and the next one starts
+// where it ends, so finding the messages is inherently sequential.  Walking it one message
+// per LDS round trip on one wave per set runs at ~0.1 B/clk/CU (the MsgVersion 2 record
+// index shows that ceiling).  Here a whole 512-thread workgroup works on one set, a 128 KiB
+// LDS window at a time, and the chain is discovered SPECULATIVELY in parallel:
+//
+//   A. every thread owns a 256-byte segment of the window and scans it for the first
+//      position that looks like a message header (MagicByte 0/1, sane Attributes and
+//      MessageSize, and the message after it also looking like one with a larger Offset);
+//      thread 0's segment starts at the window base, which is a true message start;
+//   B. from its guess each thread walks the chain to the first position past its segment
+//      (its "exit"), classifying every message exactly as the reader does;
+//   C. thread l links to thread m when its exit lies in m's segment AND equals m's guess.
+//      The links only go forward, so binary lifting (10 levels of pointer doubling in LDS)
+//      gives every thread, in O(log) steps, whether it lies on the path from thread 0 --
+//      i.e. whether its guess is a true message start.  The heuristic only decides speed,
+//      never results: a wrong or missing guess ends the verified path there, and the next
+//      window starts at the last verified exit (thread 0 is always exact, so every window
+//      advances);
+//   D. a block prefix sum over the verified threads' message counts numbers the rows; each
+//      verified thread computes the CRC-32 of its own messages from LDS (slicing-by-4).
+// A message larger than the window is computed by the whole workgroup from global memory
+// (per-thread chunks combined with x^(8n) mod P shifts).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "common.h"
+
+namespace rdk {
+namespace {
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint8_t lds_b;
+typedef __attribute__((address_space(3))) uint32_t lds_w;
+typedef __attribute__((address_space(3))) uint16_t lds_h;
+
+constexpr int kLgThreads = 512;                    // threads per set
+constexpr int kLgWaves = kLgThreads / 64;
+constexpr uint32_t kLgSeg = 256;                   // bytes scanned per thread
+constexpr uint32_t kLgWin = kLgThreads * kLgSeg;   // LDS window (128 KiB)
+constexpr int kLgLev = 10;                         // 2^10 >= kLgThreads hops
+constexpr uint32_t kNone = 0xffffffffu;
+
+// classification of the message at p (rdkafka_msgset_reader.c:566-600)
+enum : uint32_t { kOk = 0, kDone = 1, kPartial = 2, kErr = 3, kWin = 4 };
+
+struct Win {
+  const lds_b *w;  // window byte q (set offset) is w[q - base]
+  uint32_t base, end, len;  // staged [base, end) of the set's [0, len)
+  __device__ __forceinline__ uint32_t b(uint32_t q) const { return w[q - base]; }
+  // big-endian u32 at any q: two aligned LDS dwords and one v_alignbyte
+  __device__ __forceinline__ uint32_t be32(uint32_t q) const {
+    const uint32_t i = uint32_t(reinterpret_cast<uintptr_t>(w + (q - base)));
+    const lds_w *a = reinterpret_cast<const lds_w *>(w + (q - base) - (i & 3u));
+    return __builtin_bswap32(__builtin_amdgcn_alignbyte(a[1], a[0], i & 3u));
+  }
+  // MessageSize at p when the message at p is whole in the window, else the class
+  __device__ __forceinline__ uint32_t classify(uint32_t p, uint32_t &S) const {
+    if (p == len) return kDone;
+    const uint32_t R = len - p;
+    if (R < 16u) return kPartial;                     // Offset, MessageSize, Crc :566-570
+    if (p + 16u > end) return kWin;
+    const int32_t s = int32_t(be32(p + 8u));
+    if (s < 4) return kErr;                           // see DESIGN: the reference asserts
+    if (uint32_t(s) - 4u > R - 16u) return kPartial;  // narrow_copy / check_len :571-573
+    if (R < 18u) return kPartial;                     // MagicByte, Attributes :575-576
+    if (p + 18u > end) return kWin;
+    uint32_t hdr = 6u;
+    if (b(p + 16u) == 1u) {                           // MsgVersion 1: Timestamp :578-580
+      if (R < 26u) return kPartial;
+      hdr = 14u;
+    }
+    if (uint32_t(s) < hdr) return kErr;               // MessageSize < hdrsize :590-597
+    if (p + 12u + uint32_t(s) > end) return kWin;     // not whole in the window
+    S = uint32_t(s);
+    return kOk;
+  }
+  // heuristic message-start test (phase A): never decides a result
+  __device__ __forceinline__ bool plausible(uint32_t q) const {
+    if (q + 28u > end) return false;
+    const uint32_t m = b(q + 16u), a = b(q + 17u);
+    if (m > 1u || (a & 0xf0u) || (a & 7u) > 4u) return false;
+    const uint32_t S = be32(q + 8u);
+    if (S < (m ? 14u : 6u) || S > len - q - 12u) return false;
+    const uint32_t r = q + 12u + S;
+    if (r == len) return true;
+    if (r + 28u > end) return true;  // next header not staged: first-level test only
+    const uint32_t m2 = b(r + 16u), S2 = be32(r + 8u);
+    if (m2 > 1u || S2 < (m2 ? 14u : 6u) || S2 > len - r - 12u) return false;
+    const uint64_t o1 = (uint64_t(be32(q)) << 32) | be32(q + 4u);
+    const uint64_t o2 = (uint64_t(be32(r)) << 32) | be32(r + 4u);
+    return int64_t(o2 - o1) > 0 && o2 - o1 < (uint64_t(1) << 32);  // Offsets increase
+  }
+};
+
+// slicing-by-4 CRC-32 over LDS bytes [i, e) of the window (register form, no inversions)
+__device__ __forceinline__ uint32_t crc_lds(const lds_b *w, uint32_t i, uint32_t e, uint32_t c,
+                                            const lds_w *T) {
+  const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(w + i)) & 3u;
+  uint32_t h = mis ? 4u - mis : 0u;
+  if (h > e - i) h = e - i;
+  for (uint32_t k = 0; k < h; ++k, ++i) c = T[(c ^ w[i]) & 0xffu] ^ (c >> 8);
+  for (; i + 4u <= e; i += 4u) {
+    c ^= *reinterpret_cast<const lds_w *>(w + i);
+    c = T[768 + (c & 0xffu)] ^ T[512 + ((c >> 8) & 0xffu)] ^ T[256 + ((c >> 16) & 0xffu)] ^
+        T[c >> 24];
+  }
+  for (; i < e; ++i) c = T[(c ^ w[i]) & 0xffu] ^ (c >> 8);
+  return c;
+}
+
+// same over global bytes [p, e) (the big-message path)
+__device__ __forceinline__ uint32_t crc_gbl(const uint8_t *p, const uint8_t *e, uint32_t c,
+                                            const lds_w *T) {
+  while (p < e && (reinterpret_cast<uintptr_t>(p) & 3u)) c = T[(c ^ *p++) & 0xffu] ^ (c >> 8);
+  for (; p + 4 <= e; p += 4) {
+    c ^= *reinterpret_cast<const uint32_t *>(p);
+    c = T[768 + (c & 0xffu)] ^ T[512 + ((c >> 8) & 0xffu)] ^ T[256 + ((c >> 16) & 0xffu)] ^
+        T[c >> 24];
+  }
+  while (p < e) c = T[(c ^ *p++) & 0xffu] ^ (c >> 8);
+  return c;
+}
+
+__device__ __forceinline__ uint32_t mulp(uint32_t a, uint32_t b) {  // GF(2)[x]/P, reflected
+  uint32_t m = 1u << 31, p = 0;
+  for (int i = 0; i < 32; ++i) {
+    if (a & m) p ^= b;
+    m >>= 1;
+    b = (b & 1u) ? (b >> 1) ^ 0xedb88320u : b >> 1;
+  }
+  return p;
+}
+
+__device__ __forceinline__ uint32_t xpow8(uint64_t nbytes, const uint32_t *x2n) {
+  uint32_t p = 1u << 31;
+  int k = 3;
+  for (uint64_t n = nbytes; n; n >>= 1, ++k)
+    if (n & 1u) p = mulp(x2n[k], p);
+  return p;
+}
+
+__device__ __forceinline__ void put_be32(uint8_t *p, uint32_t v) {
+  p[0] = uint8_t(v >> 24);
+  p[1] = uint8_t(v >> 16);
+  p[2] = uint8_t(v >> 8);
+  p[3] = uint8_t(v);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
+    uint8_t *__restrict__ sbase, const uint64_t *__restrict__ set_offs,
+    const uint32_t *__restrict__ set_lens, const uint64_t *__restrict__ row_offs,
+    const uint32_t *__restrict__ row_caps, uint32_t *__restrict__ msg_pos,
+    uint32_t *__restrict__ msg_out, int32_t *__restrict__ count,
+    const uint32_t *__restrict__ gtab, const uint32_t *__restrict__ x2n) {
+  __shared__ __attribute__((aligned(16))) uint8_t win_s[kLgWin + 64];
+  __shared__ uint16_t J_s[kLgLev][kLgThreads];
+  __shared__ uint32_t T_s[1024];
+  __shared__ uint32_t cand_s[kLgThreads];
+  __shared__ uint32_t wsum_s[kLgWaves];
+  __shared__ uint32_t term_s[2];  // exit and class of the path's last thread
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  for (uint32_t i = t; i < 1024u; i += kLgThreads) T_s[i] = gtab[i];  // slicing tables 0..3
+  const lds_w *T = (const lds_w *)T_s;
+  const uint32_t si = blockIdx.x;
+  uint8_t *set = sbase + set_offs[si];
+  const uint32_t len = set_lens[si];
+  const uint64_t row0 = row_offs[si];
+  const uint32_t cap = row_caps[si];
+  uint32_t pos = 0, nrow = 0;
+  int32_t res = 0;
+  bool run = true;
+  while (run) {
+    // ---- stage [base, end): 16-byte buffer loads from the aligned address below base
+    const uint32_t base = pos;
+    const uintptr_t ga = reinterpret_cast<uintptr_t>(set + base);
+    const uintptr_t al = ga & ~uintptr_t(15);
+    const uint32_t sh = uint32_t(ga - al);
+    const uint32_t avail = len - base;
+    const uint32_t wl = avail < kLgWin - sh ? avail : kLgWin - sh;
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(al), 0,
+                                                        int((sh + wl + 3u) & ~3u), 0x00020000);
+    __syncthreads();  // the previous window's readers are done
+    {
+      constexpr int kV = int(kLgWin / (kLgThreads * 16));
+      u32x4 v[kV];
+#pragma unroll
+      for (int it = 0; it < kV; ++it)
+        v[it] = __builtin_amdgcn_raw_buffer_load_b128(rs, (t + kLgThreads * it) * 16u, 0, 0);
+#pragma unroll
+      for (int it = 0; it < kV; ++it)
+        *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(
+            (lds_b *)win_s + (t + kLgThreads * it) * 16u) = v[it];
+    }
+    Win W;
+    W.w = (const lds_b *)win_s + sh;
+    W.base = base;
+    W.end = base + wl;
+    W.len = len;
+    __syncthreads();
+    // ---- A: guess the first message start in this thread's segment
+    const uint32_t s0 = base + t * kLgSeg, s1 = s0 + kLgSeg;
+    uint32_t c = kNone;
+    if (t == 0) {
+      c = base;
+    } else if (s0 < W.end) {
+      const uint32_t lim = s1 < W.end ? s1 : W.end;
+      for (uint32_t q = s0; q < lim; ++q)
+        if (W.plausible(q)) {
+          c = q;
+          break;
+        }
+    }
+    cand_s[t] = c;
+    // ---- B: walk from the guess to the first position past the segment
+    uint32_t x = c, k = 0, cls = kOk;
+    if (c != kNone) {
+      while (x < s1) {
+        uint32_t S = 0;
+        cls = W.classify(x, S);
+        if (cls != kOk) break;
+        x += 12u + S;
+        ++k;
+      }
+    }
+    __syncthreads();
+    // ---- C: link to the thread whose guess is our exit; binary lifting from thread 0
+    uint32_t nxt = t;
+    if (c != kNone && cls == kOk && x < W.end) {
+      const uint32_t m = (x - base) / kLgSeg;
+      if (m < uint32_t(kLgThreads) && cand_s[m] == x) nxt = m;
+    }
+    J_s[0][t] = uint16_t(nxt);
+    for (int lv = 1; lv < kLgLev; ++lv) {
+      __syncthreads();
+      J_s[lv][t] = J_s[lv - 1][J_s[lv - 1][t]];
+    }
+    __syncthreads();
+    uint32_t cur = 0;
+    for (int lv = kLgLev - 1; lv >= 0; --lv) {
+      const uint32_t y = J_s[lv][cur];
+      if (y <= t) cur = y;
+    }
+    const bool on = c != kNone && cur == t;
+    const bool last = on && J_s[kLgLev - 1][0] == t;
+    if (last) {
+      term_s[0] = x;
+      term_s[1] = cls;
+    }
+    // ---- D: number the rows (block exclusive scan of the verified counts)
+    const uint32_t mine = on ? k : 0u;
+    uint32_t inc = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d);
+      if (lane >= uint32_t(d)) inc += y;
+    }
+    if (lane == 63u) wsum_s[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t w = 0; w < uint32_t(kLgWaves); ++w) {
+      const uint32_t y = wsum_s[w];
+      before += w < wv ? y : 0u;
+      total += y;
+    }
+    const uint32_t rb = nrow + before + inc - mine;
+    if (on) {
+      uint32_t p = c;
+      for (uint32_t i = 0; i < k; ++i) {
+        const uint32_t S = W.be32(p + 8u);
+        const uint32_t r = rb + i;
+        if (r < cap) {
+          const uint32_t crc =
+              ~crc_lds(W.w - base, p + 16u, p + 12u + S, 0xffffffffu, T);  // :613-641
+          msg_pos[row0 + r] = p;
+          if (MODE == RDK_HIP_V2_CRC_VERIFY) {
+            msg_out[row0 + r] = W.be32(p + 12u) == crc ? 0u : 1u;  // :602-628
+          } else {
+            msg_out[row0 + r] = crc;
+            if (MODE == RDK_HIP_V2_CRC_FINALIZE) put_be32(set + p + 12u, crc);  // :640-641
+          }
+        }
+        p += 12u + S;
+      }
+    }
+    nrow += total;
+    const uint32_t tx = term_s[0], tc = term_s[1];
+    if (nrow > cap) {
+      res = -(1 + int32_t(cap));
+      run = false;
+    } else if (tc == kDone || tc == kPartial) {
+      res = int32_t(nrow);
+      run = false;
+    } else if (tc == kErr) {
+      res = -(1 + int32_t(nrow));
+      run = false;
+    } else if (tx != base) {
+      pos = tx;  // the verified path's exit: the next window starts there
+    } else {
+      // ---- a message larger than the window, at base (header staged: tc == kWin)
+      const uint32_t S = W.be32(base + 8u);
+      const uint8_t *p0 = set + base + 16u;
+      const uint64_t L = uint64_t(S) - 4u;
+      const uint64_t C = ((L + kLgThreads - 1) / kLgThreads + 3u) & ~uint64_t(3);
+      const uint64_t pad = C * kLgThreads - L;  // virtual zero bytes in front
+      const uint64_t vs = uint64_t(t) * C, ve = vs + C;
+      uint32_t term = 0;
+      if (ve > pad) {
+        const uint64_t rs0 = vs > pad ? vs - pad : 0, re0 = ve - pad;
+        const uint32_t r = crc_gbl(p0 + rs0, p0 + re0, rs0 == 0 ? 0xffffffffu : 0u, T);
+        term = mulp(xpow8(uint64_t(kLgThreads - 1u - t) * C, x2n), r);
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) term ^= __shfl_xor(term, d);
+      __syncthreads();
+      if (lane == 0) wsum_s[wv] = term;
+      __syncthreads();
+      uint32_t acc = 0;
+      for (uint32_t w = 0; w < uint32_t(kLgWaves); ++w) acc ^= wsum_s[w];
+      const uint32_t crc = ~acc;
+      if (nrow >= cap) {
+        res = -(1 + int32_t(nrow));
+        run = false;
+      } else {
+        if (t == 0) {
+          msg_pos[row0 + nrow] = base;
+          if (MODE == RDK_HIP_V2_CRC_VERIFY) {
+            msg_out[row0 + nrow] = W.be32(base + 12u) == crc ? 0u : 1u;
+          } else {
+            msg_out[row0 + nrow] = crc;
+            if (MODE == RDK_HIP_V2_CRC_FINALIZE) put_be32(set + base + 12u, crc);
+          }
+        }
+        nrow += 1;
+        pos = base + 12u + S;
+      }
+    }
+    if (run && pos >= len) {  // (the walk reports kDone at len; kept for safety)
+      res = int32_t(nrow);
+      run = false;
+    }
+  }
+  if (t == 0) count[si] = res;
+}
+
+}  // namespace
+}  // namespace rdk
+
+using namespace rdk;
+
+RDK_API int rdk_hip_msgset_v01_crc(void *d_base, const uint64_t *d_set_offs,
+                                   const uint32_t *d_set_lens, const uint64_t *d_row_offs,
+                                   const uint32_t *d_row_caps, uint32_t *d_msg_pos,
+                                   uint32_t *d_msg_out, int32_t *d_count, uint32_t n, int mode,
+                                   void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_base || !d_set_offs || !d_set_lens || !d_row_offs || !d_row_caps || !d_msg_pos ||
+      !d_msg_out || !d_count)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint8_t *b = static_cast<uint8_t *>(d_base);
+  const uint32_t *tab = crc_tables_dev(c->device, kCrcKind32);
+  const uint32_t *x2n = crc_x2n_dev(c->device, kCrcKind32);
+#define RDK_V01(M)                                                                        \
+  hipLaunchKernelGGL(v01_crc_kernel<M>, dim3(n), dim3(kLgThreads), 0, s, b, d_set_offs,   \
+                     d_set_lens, d_row_offs, d_row_caps, d_msg_pos, d_msg_out, d_count, tab, \
+                     x2n)
+  switch (mode) {
+    case RDK_HIP_V2_CRC_COMPUTE: RDK_V01(RDK_HIP_V2_CRC_COMPUTE); break;
+    case RDK_HIP_V2_CRC_FINALIZE: RDK_V01(RDK_HIP_V2_CRC_FINALIZE); break;
+    case RDK_HIP_V2_CRC_VERIFY: RDK_V01(RDK_HIP_V2_CRC_VERIFY); break;
+    default: return set_error(RDK_HIP_E_INVAL, "mode %d", mode);
+  }
+#undef RDK_V01
+  RDK_HIP_CHECK(hipGetLastError());
+  return RDK_HIP_OK;
+}

@@ -17,17 +17,18 @@
 
 namespace rdk {
 int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
-                      uint32_t *d_scratch, hipStream_t s);
+                      uint32_t *d_scratch, hipStream_t s, int kind);
 uint32_t crc_scratch_words(uint64_t len);
 
-// CRC32C of `len` bytes already gathered in c->h_stage.
-static int crc_staged(Ctx *c, size_t len, uint32_t init, uint32_t *out) {
+// CRC32C (kind kCrcKind32C) or CRC-32 (kCrcKind32) of `len` bytes already gathered in
+// c->h_stage.
+static int crc_staged(Ctx *c, size_t len, uint32_t init, uint32_t *out, int kind) {
   const uint32_t words = crc_scratch_words(len);
   int rc;
   if ((rc = ensure_dev(c, 0, len + 64)) || (rc = ensure_desc(c, size_t(words) * 4))) return rc;
   if (len) RDK_HIP_CHECK(hipMemcpyAsync(c->d_stage[0], c->h_stage, len, hipMemcpyHostToDevice, c->stream));
   if ((rc = crc_device_buffer(c, c->d_stage[0], len, init,
-                              reinterpret_cast<uint32_t *>(c->d_desc), c->stream)))
+                              reinterpret_cast<uint32_t *>(c->d_desc), c->stream, kind)))
     return rc;
   RDK_HIP_CHECK(hipMemcpyAsync(c->h_desc, c->d_desc + size_t(words - 1) * 4, 4,
                                hipMemcpyDeviceToHost, c->stream));
@@ -54,16 +55,16 @@ RDK_API uint32_t crc32c(uint32_t crc, const void *buf, size_t len) {
   if (ensure_host(c, len)) fatal("crc32c: pinned staging");
   std::memcpy(c->h_stage, buf, len);
   uint32_t out = 0;
-  if (crc_staged(c, len, crc, &out)) fatal("crc32c");
+  if (crc_staged(c, len, crc, &out, kCrcKind32C)) fatal("crc32c");
   return out;
 }
 
-RDK_API uint32_t rd_slice_crc32c(rd_slice_t *slice) {
-  Ctx *c = ctx_or_die("rd_slice_crc32c");
+// iovec gather (the rdbuf.c:1099-1101 / :1118-1119 loops) into the pinned staging buffer;
+// chaining the CRC over segments == one CRC over their concatenation
+static uint32_t slice_crc(rd_slice_t *slice, int kind, const char *who) {
+  Ctx *c = ctx_or_die(who);
   const size_t total = slice_remains(slice);
-  if (ensure_host(c, total ? total : 1)) fatal("rd_slice_crc32c: pinned staging");
-  // iovec gather (rdbuf.c:1118-1119 loop) into the pinned staging buffer;
-  // chaining crc32c over segments == one crc32c over their concatenation
+  if (ensure_host(c, total ? total : 1)) fatal(who);
   size_t of = 0, rlen;
   const void *p;
   while ((rlen = slice_reader(slice, &p))) {
@@ -71,8 +72,19 @@ RDK_API uint32_t rd_slice_crc32c(rd_slice_t *slice) {
     of += rlen;
   }
   uint32_t out = 0;
-  if (crc_staged(c, of, 0u, &out)) fatal("rd_slice_crc32c");
+  if (crc_staged(c, of, 0u, &out, kind)) fatal(who);
   return out;
+}
+
+RDK_API uint32_t rd_slice_crc32c(rd_slice_t *slice) {
+  return slice_crc(slice, kCrcKind32C, "rd_slice_crc32c");
+}
+
+// rdbuf.c:1093-1104: rd_crc32_init/update/finalize, i.e. zlib crc32(0, ...) over the slice
+// (rdcrc32.h:93-131, WITH_ZLIB) -- the MsgVersion 0/1 check.crcs site
+// (rdkafka_msgset_reader.c:606)
+RDK_API uint32_t rd_slice_crc32(rd_slice_t *slice) {
+  return slice_crc(slice, kCrcKind32, "rd_slice_crc32");
 }
 
 // ------------------------------------------------------------------- LZ4F

@@ -87,6 +87,13 @@ def lib():
                                                     C.c_int32, C.c_int16, vp]
         L.or_msgset_v2_index.restype = C.c_long
         L.or_msgset_v2_index.argtypes = [vp, C.c_size_t, C.c_int64, C.c_int64] + [vp] * 8 + [C.c_long]
+        L.or_crc32.restype = C.c_uint32
+        L.or_crc32.argtypes = [C.c_uint32, vp, C.c_size_t]
+        L.or_msgset_v01_write.restype = C.c_size_t
+        L.or_msgset_v01_write.argtypes = [vp] * 6 + [C.c_uint32, C.c_uint32, C.c_int, C.c_int64,
+                                                    C.c_int8, vp]
+        L.or_msgset_v01_crc.restype = C.c_long
+        L.or_msgset_v01_crc.argtypes = [vp, C.c_size_t, C.c_int, vp, vp, C.c_long]
         _lib = L
     return _lib
 
@@ -322,3 +329,38 @@ def msgset_v2_index(records: bytes, base_offset: int = 0, base_ts: int = 0, max_
         _np_ptr(rec), len(records), base_offset, base_ts, *(_np_ptr(rows[k]) for k in
         ("offset", "timestamp", "key_off", "key_len", "val_off", "val_len", "hdr_off", "hdr_len")), m)
     return n, {k: v[:max(n, 0)] for k, v in rows.items()}
+
+
+# ------------------------------------------------------------ MsgVersion 0/1
+def crc32(crc: int, data: bytes) -> int:
+    """zlib crc32() as the reference uses it (rdcrc32.h:93-131, WITH_ZLIB)."""
+    return lib().or_crc32(crc & 0xFFFFFFFF, _buf(data), len(data))
+
+
+def msgset_v01_write(msgs: dict, first: int, cnt: int, magic: int = 1, base_offset: int = 0,
+                     attributes: int = 0) -> bytes:
+    """Uncompressed MsgVersion 0/1 MessageSet of messages [first, first+cnt)
+    (rdkafka_msgset_writer.c:583-645), CRCs filled in."""
+    import numpy as np
+    kl, vl = msgs["key_len"], msgs["val_len"]
+    cap = int(cnt) * 34 + int(np.maximum(kl[first:first + cnt], 0).sum()) + \
+        int(np.maximum(vl[first:first + cnt], 0).sum())
+    out = np.zeros(max(cap, 1), dtype=np.uint8)
+    n = lib().or_msgset_v01_write(
+        _np_ptr(msgs["arena"]), _np_ptr(msgs["ts"]), _np_ptr(msgs["key_off"]), _np_ptr(kl),
+        _np_ptr(msgs["val_off"]), _np_ptr(vl), first, cnt, magic, base_offset, attributes,
+        _np_ptr(out))
+    return bytes(out[:n])
+
+
+def msgset_v01_crc(mset: bytes, mode: int = 0, max_rows=None):
+    """Reader walk + check.crcs (rdkafka_msgset_reader.c:538-628) over one MessageSet ->
+    (n, pos, out, set_after); n < 0: message -n-1 failed the header checks."""
+    import numpy as np
+    m = max_rows if max_rows is not None else max(1, len(mset) // 18 + 1)
+    buf = np.frombuffer(bytes(mset) + b"\0", dtype=np.uint8).copy()
+    pos = np.zeros(max(m, 1), dtype=np.uint32)
+    out = np.zeros(max(m, 1), dtype=np.uint32)
+    n = lib().or_msgset_v01_crc(_np_ptr(buf), len(mset), mode, _np_ptr(pos), _np_ptr(out), m)
+    k = max(n, 0) if n >= 0 else -n - 1
+    return n, pos[:k], out[:k], bytes(buf[:len(mset)])

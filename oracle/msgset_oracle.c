@@ -161,3 +161,109 @@ long or_msgset_v2_index(const uint8_t *rec, size_t len, int64_t base_offset, int
   }
   return i;
 }
+
+/* ======================================================================
+ * MsgVersion 0/1.
+ *
+ *   CRC-32     rdcrc32.h:93-131; the reference is configured WITH_ZLIB, so this is zlib's
+ *              crc32() (reflected 0xedb88320, ~0 in and out, chainable).  Restated here as
+ *              the table-driven form of rdcrc32.h:108-117 / rdcrc32.c (crc_table).  Pinned
+ *              by the standard check value and by the system zlib (the library the
+ *              reference links) in tests/test_oracle_legacy.py.
+ *   writer     rd_kafka_msgset_writer_write_msg_v0_1 rdkafka_msgset_writer.c:583-645
+ *   reader     rd_kafka_msgset_reader_msg_v0_1 rdkafka_msgset_reader.c:538-628 (header reads,
+ *              hdrsize check, partial-message check, check.crcs)
+ * ====================================================================== */
+static uint32_t crc32_tab[256];
+static int crc32_tab_ok;
+
+static void crc32_tab_init(void) {
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t r = b;
+    for (int i = 0; i < 8; ++i) r = (r >> 1) ^ ((r & 1u) ? 0xedb88320u : 0u);
+    crc32_tab[b] = r;
+  }
+  crc32_tab_ok = 1;
+}
+
+/* zlib crc32(crc, buf, len) */
+uint32_t or_crc32(uint32_t crc, const void *buf, size_t len) {
+  const uint8_t *p = (const uint8_t *)buf;
+  if (!crc32_tab_ok) crc32_tab_init();
+  crc = ~crc;
+  while (len--) crc = crc32_tab[(crc ^ *p++) & 0xffu] ^ (crc >> 8);
+  return ~crc;
+}
+
+static uint32_t rd_be32(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* Messages [first, first+cnt) as one uncompressed MsgVersion `magic` (0 or 1) MessageSet;
+ * Offset = base_offset + k (write_msg(..., msgcnt, ...)).  Returns the set size. */
+size_t or_msgset_v01_write(const uint8_t *arena, const int64_t *ts, const uint64_t *key_off,
+                           const int32_t *key_len, const uint64_t *val_off,
+                           const int32_t *val_len, uint32_t first, uint32_t cnt, int magic,
+                           int64_t base_offset, int8_t attributes, uint8_t *out) {
+  size_t pos = 0;
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const uint32_t m = first + k;
+    const int32_t kl = key_len[m], vl = val_len[m];
+    const uint32_t kb = kl > 0 ? (uint32_t)kl : 0, vb = vl > 0 ? (uint32_t)vl : 0;
+    const uint32_t size = 4 + 1 + 1 + 4 + kb + 4 + vb + (magic == 1 ? 8 : 0); /* :598-604 */
+    uint8_t *p = out + pos;
+    be64(p, (uint64_t)(base_offset + k));                 /* Offset :594 */
+    be32(p + 8, size);                                    /* MessageSize :606 */
+    uint8_t *q = p + 16;
+    *q++ = (uint8_t)magic;                                /* MagicByte :620 */
+    *q++ = (uint8_t)attributes;                           /* Attributes :623 */
+    if (magic == 1) { be64(q, (uint64_t)ts[m]); q += 8; } /* Timestamp :626-627 */
+    be32(q, (uint32_t)(kl >= 0 ? kl : -1)); q += 4;       /* Key :630 */
+    if (kb) { memcpy(q, arena + key_off[m], kb); q += kb; }
+    be32(q, (uint32_t)(vl >= 0 ? vl : -1)); q += 4;       /* Value :633-637 */
+    if (vb) { memcpy(q, arena + val_off[m], vb); q += vb; }
+    be32(p + 12, or_crc32(0, p + 16, size - 4));          /* Crc :613-616, :639-641 */
+    pos += 12 + size;
+  }
+  return pos;
+}
+
+/* The reader's message walk + check.crcs over one MessageSet [0, len):
+ *   mode 0 COMPUTE : out[k] = CRC-32 of message k's [16, 12+MessageSize)
+ *   mode 1 FINALIZE: also stores it big-endian at the message's Crc field
+ *   mode 2 VERIFY  : out[k] = (stored == computed) ? 0 : 1 (the reader continues)
+ * pos[k] = message start.  Returns the number of whole messages (a partial message at
+ * the end stops the walk, :599-600 / UNDERFLOW), or -(1+k) when message k fails the
+ * header checks (MessageSize < hdrsize :590-597; MessageSize < 4, where the reference's
+ * rd_slice_narrow_copy asserts) or does not fit in max_rows. */
+long or_msgset_v01_crc(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32_t *out,
+                       long max_rows) {
+  size_t p = 0;
+  long k = 0;
+  while (p < len) {
+    const size_t R = len - p;
+    if (R < 16) return k;                          /* Offset, MessageSize, Crc :566-570 */
+    const int32_t S = (int32_t)rd_be32(set + p + 8);
+    if (S < 4) return -(1 + k);
+    if ((size_t)(S - 4) > R - 16) return k;        /* narrow_copy + check_len :571-573 */
+    if (R < 18) return k;                          /* MagicByte, Attributes :575-576 */
+    size_t hdr = 6;
+    if (set[p + 16] == 1) {                        /* Timestamp :578-580 */
+      if (R < 26) return k;
+      hdr = 14;
+    }
+    if ((size_t)S < hdr) return -(1 + k);          /* :590-597 */
+    if (k >= max_rows) return -(1 + k);
+    const uint32_t crc = or_crc32(0, set + p + 16, (size_t)S - 4);
+    pos[k] = (uint32_t)p;
+    if (mode == 2) {
+      out[k] = rd_be32(set + p + 12) == crc ? 0u : 1u;   /* :602-628 */
+    } else {
+      out[k] = crc;
+      if (mode == 1) be32(set + p + 12, crc);
+    }
+    p += 12 + (size_t)S;
+    ++k;
+  }
+  return k;
+}

@@ -115,6 +115,16 @@ long     or_msgset_v2_index(const uint8_t *rec, size_t len, int64_t base_offset,
                             int32_t *val_len, uint32_t *hdr_off, uint32_t *hdr_len,
                             long max_rows);
 
+/* ---- MsgVersion 0/1 (msgset_oracle.c) ------------------------------------ */
+/* zlib crc32() (rdcrc32.h:93-131 WITH_ZLIB), chainable. */
+uint32_t or_crc32(uint32_t crc, const void *buf, size_t len);
+size_t or_msgset_v01_write(const uint8_t *arena, const int64_t *ts, const uint64_t *key_off,
+                           const int32_t *key_len, const uint64_t *val_off,
+                           const int32_t *val_len, uint32_t first, uint32_t cnt, int magic,
+                           int64_t base_offset, int8_t attributes, uint8_t *out);
+long or_msgset_v01_crc(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32_t *out,
+                       long max_rows);
+
 #ifdef __cplusplus
 }
 #endif

@@ -325,6 +325,70 @@ def bench_index(args, rank, world, n=None, per_batch=9500):
             "host_sample": (base, per_batch)}
 
 
+def bench_legacy(args, rank, world, n=None, set_bytes=1 << 20):
+    """MsgVersion 1 MessageSets (~1 MiB of ~150-byte JSON messages each)
+    through the consumer's per-message check.crcs (rd_kafka_msgset_reader_msg_v0_1,
+    rdkafka_msgset_reader.c:566-628: message walk + CRC-32 of [16, 12+MessageSize)).
+    The sets are laid out on the host, tiled, and given their CRCs by the engine's FINALIZE
+    (the writer side, rdkafka_msgset_writer.c:613-641) before the timed VERIFY steps."""
+    import numpy as np
+    import torch
+    import librdkafka_amd as L
+    from librdkafka_amd import workload as W
+    n = n or args.partitions // world
+    base = W.gen_messages(16384, seed=42 + rank)
+    one = W.msgset_v01_bytes(base, 0, 16384, magic=1, max_bytes=set_bytes)
+    msgs = 0
+    p = 0
+    while p < len(one):
+        p += 12 + int.from_bytes(one[p + 8:p + 12], "big")
+        msgs += 1
+    sz = len(one)
+    buf = torch.from_numpy(np.frombuffer(one, dtype=np.uint8).copy()).cuda().repeat(n)
+    offs = torch.arange(n, dtype=torch.int64, device="cuda") * sz
+    lens = torch.full((n,), sz, dtype=torch.int32, device="cuda")
+    row_offs = torch.arange(n, dtype=torch.int64, device="cuda") * msgs
+    caps = torch.full((n,), msgs, dtype=torch.int32, device="cuda")
+    pos = torch.empty(n * msgs, dtype=torch.int32, device="cuda")
+    out = torch.empty(n * msgs, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(n, dtype=torch.int32, device="cuda")
+    run = lambda mode: L.msgset_v01_crc(buf, offs, lens, row_offs, caps, pos, out, cnt, mode)
+    fin_ms, fin_kms = _timed(lambda: run(L.V2_CRC_FINALIZE), 1, 0, world)
+    ms, kms = _timed(lambda: run(L.V2_CRC_VERIFY), args.steps, args.warmup, world)
+    assert bool((cnt == msgs).all()) and int(out.abs().sum()) == 0
+    total = n * sz
+    return {"ms": ms, "kernel_ms": kms, "bytes": total, "records": n,
+            "alg_bytes": total + 8 * n * msgs, "finalize_kernel_ms": round(fin_kms, 3),
+            "host_sample": (one, msgs)}
+
+
+def cpu_baseline_legacy(one, msgs, seconds=3.0):
+    """The reader walk restated (msgset_oracle.c) with the system zlib's crc32() -- the
+    CRC function the reference itself calls (rdcrc32.h, WITH_ZLIB) -- one host thread."""
+    import numpy as np
+    import oracle
+    import librdkafka_amd as L
+    # fill the CRCs the way the writer does, then time VERIFY passes
+    st = np.frombuffer(one, dtype=np.uint8).copy()
+    pos = np.zeros(msgs, dtype=np.uint32)
+    out = np.zeros(msgs, dtype=np.uint32)
+    lib = oracle.lib()
+    assert lib.or_msgset_v01_crc_zlib(st.ctypes.data, len(one), L.V2_CRC_FINALIZE,
+                                      pos.ctypes.data, out.ctypes.data, msgs) == msgs
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        assert lib.or_msgset_v01_crc_zlib(st.ctypes.data, len(one), L.V2_CRC_VERIFY,
+                                          pos.ctypes.data, out.ctypes.data, msgs) == msgs
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(passes * len(one) / el / 1e9, 3), "unit": "GB/s", "cores": 1,
+            "kind": "reference", "sample": f"{passes} VERIFY passes over one MsgVersion 1 set "
+            f"({msgs} JSON messages, {len(one)} B): reader walk restated, zlib crc32() "
+            f"(the reference's CRC-32), {cpu_model()}"}
+
+
 def cpu_baseline_index(base, per_batch, seconds=3.0):
     """The oracle restatement of rd_kafka_msgset_reader_msg_v2 (msgset_oracle.c), one host
     thread, over a batch of the same messages."""
@@ -540,6 +604,15 @@ def index_leg(rank, world, no_cpu):
     return leg_line("index", res, 3, world, cpu)
 
 
+def legacy_leg(rank, world, no_cpu):
+    res = bench_legacy(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
+    cpu = None if no_cpu else cpu_baseline_legacy(*res.pop("host_sample"))
+    res.pop("host_sample", None)
+    d = leg_line("legacy", res, 3, world, cpu)
+    d["finalize_kernel_ms"] = res["finalize_kernel_ms"]
+    return d
+
+
 def serialize_leg(rank, world, no_cpu):
     res = bench_serialize(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
     cpu = None if no_cpu else cpu_baseline_serialize(*res.pop("host_sample"))
@@ -576,7 +649,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="crc",
                     choices=["crc", "lz4c", "lz4c_fast", "consumer", "producer", "serialize",
-                             "index"])
+                             "index", "legacy"])
     ap.add_argument("--batches", type=int, default=CRC_BATCHES)
     ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -603,6 +676,8 @@ def main():
             res = bench_serialize(args, rank, world)
         elif args.workload == "index":
             res = bench_index(args, rank, world)
+        elif args.workload == "legacy":
+            res = bench_legacy(args, rank, world)
         else:
             res = bench_consumer(args, rank, world)
         t_max = max_over_ranks(res["ms"], world)
@@ -613,6 +688,8 @@ def main():
                     cpu = cpu_baseline_serialize(*res["host_sample"])
                 elif args.workload == "index":
                     cpu = cpu_baseline_index(*res["host_sample"])
+                elif args.workload == "legacy":
+                    cpu = cpu_baseline_legacy(*res["host_sample"])
                 else:
                     cpu = cpu_baseline_lz4("decompress" if args.workload == "consumer"
                                            else "compress")
@@ -680,6 +757,7 @@ def main():
                                                rank, world), 3, 1, cpu("decompress")),
                 "v2_record_serialize_1MiB_json": serialize_leg(rank, world, args.no_cpu_baseline),
                 "v2_record_index_1MiB_json": index_leg(rank, world, args.no_cpu_baseline),
+                "v1_msgset_crc32_verify_1MiB_json": legacy_leg(rank, world, args.no_cpu_baseline),
                 "producer_pipeline_1MiB_json_pcie": leg_line(
                     "producer", bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512),
                                                rank, world), 2, 1, cpu("compress")),

@@ -11,12 +11,13 @@
 // A MessageSet is a chain: message p is [p, p + 12 + MessageSize) and the next one starts
 // where it ends, so finding the messages is inherently sequential.  Walking it one message
 // per LDS round trip on one wave per set runs at ~0.1 B/clk/CU (the MsgVersion 2 record
-// index shows that ceiling).  Here a whole 512-thread workgroup works on one set, a 128 KiB
+// index shows that ceiling).  Here a whole 512-thread workgroup works on one set, a 130 KiB
 // LDS window at a time, and the chain is discovered SPECULATIVELY in parallel:
 //
-//   A. every thread owns a 256-byte segment of the window and scans it for the first
-//      position that looks like a message header (MagicByte 0/1, sane Attributes and
-//      MessageSize, and the message after it also looking like one with a larger Offset);
+//   A. every thread owns a 260-byte segment of the window and scans it for the first
+//      position that looks like a message header (MagicByte 0/1, sane Attributes, a
+//      MessageSize that its Key and Value length fields fill exactly, and the message after
+//      it also looking like one, with a larger Offset);
 //      thread 0's segment starts at the window base, which is a true message start;
 //   B. from its guess each thread walks the chain to the first position past its segment
 //      (its "exit"), classifying every message exactly as the reader does;
@@ -28,11 +29,12 @@
 //      window starts at the last verified exit (thread 0 is always exact, so every window
 //      advances);
 //   D. a block prefix sum over the verified threads' message counts numbers the rows; each
-//      verified thread computes the CRC-32 of its own messages from LDS (slicing-by-4).
+//      verified thread computes the CRC-32 of its own messages from LDS (slicing-by-8).
 // A message larger than the window is computed by the whole workgroup from global memory
 // (per-thread chunks combined with x^(8n) mod P shifts).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstring>
 
 #include "common.h"
@@ -48,8 +50,11 @@ typedef __attribute__((address_space(3))) uint16_t lds_h;
 
 constexpr int kLgThreads = 512;                    // threads per set
 constexpr int kLgWaves = kLgThreads / 64;
-constexpr uint32_t kLgSeg = 256;                   // bytes scanned per thread
-constexpr uint32_t kLgWin = kLgThreads * kLgSeg;   // LDS window (128 KiB)
+// bytes scanned per thread: 65 dwords, so the 64 lanes of a wave, which scan in lockstep
+// from the same offset of their segments, hit 64 different LDS banks (a 256-byte stride
+// put them all in one bank)
+constexpr uint32_t kLgSeg = 260;
+constexpr uint32_t kLgWin = kLgThreads * kLgSeg;   // LDS window (130 KiB)
 constexpr int kLgLev = 10;                         // 2^10 >= kLgThreads hops
 constexpr uint32_t kNone = 0xffffffffu;
 
@@ -59,6 +64,7 @@ enum : uint32_t { kOk = 0, kDone = 1, kPartial = 2, kErr = 3, kWin = 4 };
 struct Win {
   const lds_b *w;  // window byte q (set offset) is w[q - base]
   uint32_t base, end, len;  // staged [base, end) of the set's [0, len)
+  uint32_t q_idx0;          // LDS address of window byte base (w)
   __device__ __forceinline__ uint32_t b(uint32_t q) const { return w[q - base]; }
   // big-endian u32 at any q: two aligned LDS dwords and one v_alignbyte
   __device__ __forceinline__ uint32_t be32(uint32_t q) const {
@@ -87,35 +93,110 @@ struct Win {
     S = uint32_t(s);
     return kOk;
   }
-  // heuristic message-start test (phase A): never decides a result
+  // first q in [s0, lim) passing plausible(), or kNone.  Sixteen candidates i..i+15 per
+  // step, tested bytewise (SWAR) on a sliding run of aligned LDS dwords D[k] = bytes
+  // i+4k..i+4k+3: bytes q, q+1 (Offset's top bytes: offsets < 2^48), q+8 (MessageSize's
+  // top byte: < 16 MiB), q+16 (MagicByte <= 1) and q+17 (Attributes < 8).  Four new dwords
+  // per step, loaded a step ahead.  Rounds: every lane first advances (no dependent
+  // loads) to its next surviving candidate, then all lanes run the full test together, so
+  // the wave pays one full test per round rather than one per step in which any lane has
+  // a survivor.
+  __device__ __forceinline__ uint32_t scan(uint32_t s0, uint32_t lim) const {
+    const lds_b *w0 = w - (q_idx0 & 15u);  // 16-byte aligned window start
+    const uint32_t off = (q_idx0 & 15u) - base;  // LDS index of q = q + off
+    auto W32 = [&](uint32_t i) { return *reinterpret_cast<const lds_w *>(w0 + i); };
+    auto zb = [](uint32_t x) { return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u; };
+    uint32_t i = (s0 + off) & ~3u;
+    const uint32_t ie = lim + off;
+    uint32_t D[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) D[k] = W32(i + 4u * k);
+    uint64_t mlo = 0, mhi = 0;  // survivors of candidates mi..mi+7 / mi+8..mi+15
+    uint32_t mi = i;
+    for (;;) {
+      while (!(mlo | mhi) && i < ie) {
+        uint32_t N[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) N[k] = W32(i + 40u + 4u * k);  // next step's D[6..9]
+        uint32_t g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          g[k] = zb(D[k]) & zb(__builtin_amdgcn_alignbyte(D[k + 1], D[k], 1u)) & zb(D[k + 2]) &
+                 zb(D[k + 4] & 0xfefefefeu) &
+                 zb(__builtin_amdgcn_alignbyte(D[k + 5], D[k + 4], 1u) & 0xf8f8f8f8u);
+        mlo = g[0] | (uint64_t(g[1]) << 32);
+        mhi = g[2] | (uint64_t(g[3]) << 32);
+        mi = i;
+        i += 16u;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) D[k] = D[k + 4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) D[6 + k] = N[k];
+      }
+      if (!(mlo | mhi)) break;
+      uint32_t bit;
+      if (mlo) {
+        bit = uint32_t(__builtin_ctzll(mlo));
+        mlo &= mlo - 1u;
+      } else {
+        bit = 64u + uint32_t(__builtin_ctzll(mhi));
+        mhi &= mhi - 1u;
+      }
+      const uint32_t q = mi + 4u * (bit >> 5) + ((bit & 31u) >> 3) - off;
+      if (q >= s0 && q < lim && plausible(q)) return q;
+    }
+    return kNone;
+  }
+  // heuristic message-start test (phase A): never decides a result.  Branch-free in two
+  // rounds of independent LDS loads (the candidate's fields, then the ones their values
+  // point at), so a test costs two LDS round trips.
   __device__ __forceinline__ bool plausible(uint32_t q) const {
-    if (q + 28u > end) return false;
-    const uint32_t m = b(q + 16u), a = b(q + 17u);
-    if (m > 1u || (a & 0xf0u) || (a & 7u) > 4u) return false;
-    const uint32_t S = be32(q + 8u);
-    if (S < (m ? 14u : 6u) || S > len - q - 12u) return false;
+    if (q + 34u > end) return false;
+    // round 1: Offset, MessageSize, MagicByte/Attributes, KeyLength (v0 at +18, v1 at +26)
+    const uint32_t o1h = be32(q), o1l = be32(q + 4u), S = be32(q + 8u), h = be32(q + 16u);
+    const uint32_t k0 = be32(q + 18u), k1 = be32(q + 26u);
+    const uint32_t m = h >> 24, a = (h >> 16) & 0xffu, hdr = m ? 14u : 6u;
+    bool ok = m <= 1u && !(a & 0xf0u) && (a & 7u) <= 4u && S >= hdr + 8u &&
+              S <= len - q - 12u;
+    const int32_t kl = int32_t(m ? k1 : k0);
+    ok = ok && kl >= -1 && (kl <= 0 || uint32_t(kl) <= S - hdr - 8u);
+    const uint32_t kb = kl > 0 ? uint32_t(kl) : 0u;
     const uint32_t r = q + 12u + S;
-    if (r == len) return true;
-    if (r + 28u > end) return true;  // next header not staged: first-level test only
-    const uint32_t m2 = b(r + 16u), S2 = be32(r + 8u);
-    if (m2 > 1u || S2 < (m2 ? 14u : 6u) || S2 > len - r - 12u) return false;
-    const uint64_t o1 = (uint64_t(be32(q)) << 32) | be32(q + 4u);
-    const uint64_t o2 = (uint64_t(be32(r)) << 32) | be32(r + 4u);
-    return int64_t(o2 - o1) > 0 && o2 - o1 < (uint64_t(1) << 32);  // Offsets increase
+    const bool at_end = r == len;
+    ok = ok && (at_end || r + 28u <= end);  // the next header must be staged too
+    // round 2: ValueLength, the next message's Offset, MessageSize, MagicByte
+    const uint32_t va = ok ? q + 16u + hdr + kb : q, ra = ok && !at_end ? r : q;
+    const int32_t vl = int32_t(be32(va));
+    const uint32_t o2h = be32(ra), o2l = be32(ra + 4u), S2 = be32(ra + 8u), m2 = b(ra + 16u);
+    // Key and Value length fields fill the message exactly (:630-637)
+    ok = ok && vl >= -1 && hdr + 8u + kb + (vl > 0 ? uint32_t(vl) : 0u) == S;
+    if (at_end) return ok;
+    const uint64_t o1 = (uint64_t(o1h) << 32) | o1l, o2 = (uint64_t(o2h) << 32) | o2l;
+    return ok && m2 <= 1u && S2 >= (m2 ? 14u : 6u) && S2 <= len - r - 12u &&
+           int64_t(o2 - o1) > 0 && o2 - o1 < (uint64_t(1) << 32);  // Offsets increase
   }
 };
 
-// slicing-by-4 CRC-32 over LDS bytes [i, e) of the window (register form, no inversions)
+// slicing-by-8 CRC-32 over LDS bytes [i, e) of the window (register form, no inversions):
+// one dependent LDS round trip per 8 bytes
 __device__ __forceinline__ uint32_t crc_lds(const lds_b *w, uint32_t i, uint32_t e, uint32_t c,
                                             const lds_w *T) {
   const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(w + i)) & 3u;
   uint32_t h = mis ? 4u - mis : 0u;
   if (h > e - i) h = e - i;
   for (uint32_t k = 0; k < h; ++k, ++i) c = T[(c ^ w[i]) & 0xffu] ^ (c >> 8);
-  for (; i + 4u <= e; i += 4u) {
+  for (; i + 8u <= e; i += 8u) {
+    const uint32_t lo = c ^ *reinterpret_cast<const lds_w *>(w + i);
+    const uint32_t hi = *reinterpret_cast<const lds_w *>(w + i + 4u);
+    c = T[1792 + (lo & 0xffu)] ^ T[1536 + ((lo >> 8) & 0xffu)] ^ T[1280 + ((lo >> 16) & 0xffu)] ^
+        T[1024 + (lo >> 24)] ^ T[768 + (hi & 0xffu)] ^ T[512 + ((hi >> 8) & 0xffu)] ^
+        T[256 + ((hi >> 16) & 0xffu)] ^ T[hi >> 24];
+  }
+  if (i + 4u <= e) {
     c ^= *reinterpret_cast<const lds_w *>(w + i);
     c = T[768 + (c & 0xffu)] ^ T[512 + ((c >> 8) & 0xffu)] ^ T[256 + ((c >> 16) & 0xffu)] ^
         T[c >> 24];
+    i += 4u;
   }
   for (; i < e; ++i) c = T[(c ^ w[i]) & 0xffu] ^ (c >> 8);
   return c;
@@ -159,6 +240,19 @@ __device__ __forceinline__ void put_be32(uint8_t *p, uint32_t v) {
   p[3] = uint8_t(v);
 }
 
+#ifdef RDK_LG_PROF  // phase timing (A/B builds only): s_memtime cycles summed over blocks
+__device__ unsigned long long g_lg_prof[8];
+#define LG_T(i)                                                          \
+  do {                                                                   \
+    __syncthreads();                                                     \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime();          \
+    if (t == 0) atomicAdd(&g_lg_prof[i], _n - prof_t);                   \
+    prof_t = _n;                                                         \
+  } while (0)
+#else
+#define LG_T(i) do { } while (0)
+#endif
+
 template <int MODE>
 __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
     uint8_t *__restrict__ sbase, const uint64_t *__restrict__ set_offs,
@@ -168,12 +262,12 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
     const uint32_t *__restrict__ gtab, const uint32_t *__restrict__ x2n) {
   __shared__ __attribute__((aligned(16))) uint8_t win_s[kLgWin + 64];
   __shared__ uint16_t J_s[kLgLev][kLgThreads];
-  __shared__ uint32_t T_s[1024];
+  __shared__ uint32_t T_s[2048];
   __shared__ uint32_t cand_s[kLgThreads];
   __shared__ uint32_t wsum_s[kLgWaves];
   __shared__ uint32_t term_s[2];  // exit and class of the path's last thread
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  for (uint32_t i = t; i < 1024u; i += kLgThreads) T_s[i] = gtab[i];  // slicing tables 0..3
+  for (uint32_t i = t; i < 2048u; i += kLgThreads) T_s[i] = gtab[i];  // slicing tables 0..7
   const lds_w *T = (const lds_w *)T_s;
   const uint32_t si = blockIdx.x;
   uint8_t *set = sbase + set_offs[si];
@@ -183,6 +277,9 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
   uint32_t pos = 0, nrow = 0;
   int32_t res = 0;
   bool run = true;
+#ifdef RDK_LG_PROF
+  unsigned long long prof_t = __builtin_amdgcn_s_memtime();
+#endif
   while (run) {
     // ---- stage [base, end): 16-byte buffer loads from the aligned address below base
     const uint32_t base = pos;
@@ -195,36 +292,35 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
                                                         int((sh + wl + 3u) & ~3u), 0x00020000);
     __syncthreads();  // the previous window's readers are done
     {
-      constexpr int kV = int(kLgWin / (kLgThreads * 16));
+      constexpr int kV = int((kLgWin + kLgThreads * 16 - 1) / (kLgThreads * 16));
       u32x4 v[kV];
 #pragma unroll
       for (int it = 0; it < kV; ++it)
         v[it] = __builtin_amdgcn_raw_buffer_load_b128(rs, (t + kLgThreads * it) * 16u, 0, 0);
 #pragma unroll
       for (int it = 0; it < kV; ++it)
-        *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(
-            (lds_b *)win_s + (t + kLgThreads * it) * 16u) = v[it];
+        if ((t + kLgThreads * it) * 16u < kLgWin)
+          *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(
+              (lds_b *)win_s + (t + kLgThreads * it) * 16u) = v[it];
     }
     Win W;
     W.w = (const lds_b *)win_s + sh;
     W.base = base;
     W.end = base + wl;
     W.len = len;
+    W.q_idx0 = uint32_t(reinterpret_cast<uintptr_t>(W.w));
     __syncthreads();
+    LG_T(0);
     // ---- A: guess the first message start in this thread's segment
     const uint32_t s0 = base + t * kLgSeg, s1 = s0 + kLgSeg;
     uint32_t c = kNone;
     if (t == 0) {
       c = base;
     } else if (s0 < W.end) {
-      const uint32_t lim = s1 < W.end ? s1 : W.end;
-      for (uint32_t q = s0; q < lim; ++q)
-        if (W.plausible(q)) {
-          c = q;
-          break;
-        }
+      c = W.scan(s0, s1 < W.end ? s1 : W.end);
     }
     cand_s[t] = c;
+    LG_T(1);
     // ---- B: walk from the guess to the first position past the segment
     uint32_t x = c, k = 0, cls = kOk;
     if (c != kNone) {
@@ -237,6 +333,7 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
       }
     }
     __syncthreads();
+    LG_T(2);
     // ---- C: link to the thread whose guess is our exit; binary lifting from thread 0
     uint32_t nxt = t;
     if (c != kNone && cls == kOk && x < W.end) {
@@ -260,6 +357,7 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
       term_s[0] = x;
       term_s[1] = cls;
     }
+    LG_T(3);
     // ---- D: number the rows (block exclusive scan of the verified counts)
     const uint32_t mine = on ? k : 0u;
     uint32_t inc = mine;
@@ -296,6 +394,11 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
         p += 12u + S;
       }
     }
+    LG_T(4);
+#ifdef RDK_LG_PROF
+    if (t == 0) atomicAdd(&g_lg_prof[6], 1ull);
+    if (t == 0) atomicAdd(&g_lg_prof[7], (unsigned long long)(term_s[0] - base));
+#endif
     nrow += total;
     const uint32_t tx = term_s[0], tc = term_s[1];
     if (nrow > cap) {
@@ -354,6 +457,9 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
     }
   }
   if (t == 0) count[si] = res;
+#ifdef RDK_LG_PROF
+  if (t == 0) atomicAdd(&g_lg_prof[5], 1ull);
+#endif
 }
 
 }  // namespace
@@ -388,5 +494,12 @@ RDK_API int rdk_hip_msgset_v01_crc(void *d_base, const uint64_t *d_set_offs,
   }
 #undef RDK_V01
   RDK_HIP_CHECK(hipGetLastError());
+#ifdef RDK_LG_PROF
+  unsigned long long h[8];
+  RDK_HIP_CHECK(hipStreamSynchronize(s));
+  RDK_HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_lg_prof), sizeof h));
+  fprintf(stderr, "lg_prof stage %llu A %llu B %llu C %llu D %llu blocks %llu windows %llu "
+          "advance %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+#endif
   return RDK_HIP_OK;
 }

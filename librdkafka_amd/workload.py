@@ -123,3 +123,26 @@ def gen_messages(n: int, seed: int = 42, headers: bool = True) -> dict:
     return {"arena": np.frombuffer(bytes(arena) or b"\0", np.uint8).copy(), "ts": ts,
             "key_off": key_off, "key_len": key_len, "val_off": val_off, "val_len": val_len,
             "hdr_off": hdr_off, "hdr_len": hdr_len, "hdr_cnt": hdr_cnt}
+
+
+def msgset_v01_bytes(msgs: dict, first: int, cnt: int, magic: int = 1,
+                     base_offset: int = 0, max_bytes: int | None = None) -> bytes:
+    """Uncompressed MsgVersion 0/1 MessageSet of messages [first, first+cnt) in the layout of
+    rd_kafka_msgset_writer_write_msg_v0_1 (rdkafka_msgset_writer.c:583-645), with the Crc
+    fields left 0: the engine's FINALIZE mode fills them.  Stops before max_bytes."""
+    arena = msgs["arena"]
+    out = bytearray()
+    for k in range(cnt):
+        m = first + k
+        kl, vl = int(msgs["key_len"][m]), int(msgs["val_len"][m])
+        kb, vb = max(kl, 0), max(vl, 0)
+        size = 4 + 1 + 1 + 4 + kb + 4 + vb + (8 if magic == 1 else 0)
+        if max_bytes is not None and len(out) + 12 + size > max_bytes:
+            break
+        out += struct.pack(">qiIbb", base_offset + k, size, 0, magic, 0)
+        if magic == 1:
+            out += struct.pack(">q", int(msgs["ts"][m]))
+        ko, vo = int(msgs["key_off"][m]), int(msgs["val_off"][m])
+        out += struct.pack(">i", kl if kl >= 0 else -1) + arena[ko:ko + kb].tobytes()
+        out += struct.pack(">i", vl if vl >= 0 else -1) + arena[vo:vo + vb].tobytes()
+    return bytes(out)

@@ -94,6 +94,8 @@ def lib():
                                                     C.c_int8, vp]
         L.or_msgset_v01_crc.restype = C.c_long
         L.or_msgset_v01_crc.argtypes = [vp, C.c_size_t, C.c_int, vp, vp, C.c_long]
+        L.or_msgset_v01_crc_zlib.restype = C.c_long
+        L.or_msgset_v01_crc_zlib.argtypes = [vp, C.c_size_t, C.c_int, vp, vp, C.c_long]
         _lib = L
     return _lib
 

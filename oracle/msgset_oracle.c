@@ -21,6 +21,7 @@
  */
 #include <stdint.h>
 #include <string.h>
+#include <zlib.h>
 
 #include "oracle.h"
 
@@ -236,8 +237,10 @@ size_t or_msgset_v01_write(const uint8_t *arena, const int64_t *ts, const uint64
  * the end stops the walk, :599-600 / UNDERFLOW), or -(1+k) when message k fails the
  * header checks (MessageSize < hdrsize :590-597; MessageSize < 4, where the reference's
  * rd_slice_narrow_copy asserts) or does not fit in max_rows. */
-long or_msgset_v01_crc(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32_t *out,
-                       long max_rows) {
+typedef uint32_t (*crc_fn)(uint32_t, const void *, size_t);
+
+static long v01_walk(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32_t *out,
+                     long max_rows, crc_fn crcf) {
   size_t p = 0;
   long k = 0;
   while (p < len) {
@@ -254,7 +257,7 @@ long or_msgset_v01_crc(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32
     }
     if ((size_t)S < hdr) return -(1 + k);          /* :590-597 */
     if (k >= max_rows) return -(1 + k);
-    const uint32_t crc = or_crc32(0, set + p + 16, (size_t)S - 4);
+    const uint32_t crc = crcf(0, set + p + 16, (size_t)S - 4);
     pos[k] = (uint32_t)p;
     if (mode == 2) {
       out[k] = rd_be32(set + p + 12) == crc ? 0u : 1u;   /* :602-628 */
@@ -266,4 +269,20 @@ long or_msgset_v01_crc(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32
     ++k;
   }
   return k;
+}
+
+long or_msgset_v01_crc(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32_t *out,
+                       long max_rows) {
+  return v01_walk(set, len, mode, pos, out, max_rows, or_crc32);
+}
+
+/* The same walk with the system zlib's crc32() -- the function the reference itself calls
+ * (rdcrc32.h WITH_ZLIB): bench.py's CPU baseline ("kind": "reference" for the CRC). */
+static uint32_t zlib_crc(uint32_t c, const void *p, size_t n) {
+  return (uint32_t)crc32(c, (const Bytef *)p, (uInt)n);
+}
+
+long or_msgset_v01_crc_zlib(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32_t *out,
+                            long max_rows) {
+  return v01_walk(set, len, mode, pos, out, max_rows, zlib_crc);
 }

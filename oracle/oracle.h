@@ -124,6 +124,9 @@ size_t or_msgset_v01_write(const uint8_t *arena, const int64_t *ts, const uint64
                            int64_t base_offset, int8_t attributes, uint8_t *out);
 long or_msgset_v01_crc(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32_t *out,
                        long max_rows);
+/* same walk, CRC through the system zlib (the reference's crc32): the CPU baseline */
+long or_msgset_v01_crc_zlib(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32_t *out,
+                            long max_rows);
 
 #ifdef __cplusplus
 }

@@ -277,32 +277,38 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
   uint32_t pos = 0, nrow = 0;
   int32_t res = 0;
   bool run = true;
+  constexpr int kV = int((kLgWin + kLgThreads * 16 - 1) / (kLgThreads * 16));
+  u32x4 pv[kV];
+  bool pref = false;
+  auto issue = [&](uint32_t b0) {  // the window at b0 into pv (bytes past the set read 0)
+    const uintptr_t ga = reinterpret_cast<uintptr_t>(set + b0);
+    const uintptr_t al = ga & ~uintptr_t(15);
+    const uint32_t sh0 = uint32_t(ga - al), av = len - b0;
+    const uint32_t wl0 = av < kLgWin - sh0 ? av : kLgWin - sh0;
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(al), 0,
+                                                        int((sh0 + wl0 + 3u) & ~3u), 0x00020000);
+#pragma unroll
+    for (int it = 0; it < kV; ++it)
+      pv[it] = __builtin_amdgcn_raw_buffer_load_b128(rs, (t + kLgThreads * it) * 16u, 0, 0);
+  };
 #ifdef RDK_LG_PROF
   unsigned long long prof_t = __builtin_amdgcn_s_memtime();
 #endif
   while (run) {
     // ---- stage [base, end): 16-byte buffer loads from the aligned address below base
+    // (issued during the previous window's CRC phase when that window could tell where
+    // this one starts), stored once the previous window's readers are done
     const uint32_t base = pos;
-    const uintptr_t ga = reinterpret_cast<uintptr_t>(set + base);
-    const uintptr_t al = ga & ~uintptr_t(15);
-    const uint32_t sh = uint32_t(ga - al);
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(set + base)) & 15u;
     const uint32_t avail = len - base;
     const uint32_t wl = avail < kLgWin - sh ? avail : kLgWin - sh;
-    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(al), 0,
-                                                        int((sh + wl + 3u) & ~3u), 0x00020000);
-    __syncthreads();  // the previous window's readers are done
-    {
-      constexpr int kV = int((kLgWin + kLgThreads * 16 - 1) / (kLgThreads * 16));
-      u32x4 v[kV];
+    if (!pref) issue(base);
+    __syncthreads();
 #pragma unroll
-      for (int it = 0; it < kV; ++it)
-        v[it] = __builtin_amdgcn_raw_buffer_load_b128(rs, (t + kLgThreads * it) * 16u, 0, 0);
-#pragma unroll
-      for (int it = 0; it < kV; ++it)
-        if ((t + kLgThreads * it) * 16u < kLgWin)
-          *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(
-              (lds_b *)win_s + (t + kLgThreads * it) * 16u) = v[it];
-    }
+    for (int it = 0; it < kV; ++it)
+      if ((t + kLgThreads * it) * 16u < kLgWin)
+        *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(
+            (lds_b *)win_s + (t + kLgThreads * it) * 16u) = pv[it];
     Win W;
     W.w = (const lds_b *)win_s + sh;
     W.base = base;
@@ -375,6 +381,11 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
       total += y;
     }
     const uint32_t rb = nrow + before + inc - mine;
+    const uint32_t tx = term_s[0], tc = term_s[1];
+    // the next window's start is known now: overlap its loads with the CRC phase
+    pref = nrow + total <= cap && tc != kDone && tc != kPartial && tc != kErr && tx != base &&
+           tx < len;
+    if (pref) issue(tx);
     if (on) {
       uint32_t p = c;
       for (uint32_t i = 0; i < k; ++i) {
@@ -400,7 +411,6 @@ __global__ __launch_bounds__(kLgThreads, 1) void v01_crc_kernel(
     if (t == 0) atomicAdd(&g_lg_prof[7], (unsigned long long)(term_s[0] - base));
 #endif
     nrow += total;
-    const uint32_t tx = term_s[0], tc = term_s[1];
     if (nrow > cap) {
       res = -(1 + int32_t(cap));
       run = false;

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "common.h"
+#include "specwalk.h"
 
 #include <cstring>
 
@@ -566,6 +567,122 @@ __global__ __launch_bounds__(64 * kIdxWaves) void v2_index_kernel(
   if (lane == 0) count[bi] = err >= 0 ? -(1 + err) : int32_t(nrow);
 }
 
+// ---- the default record index: one 512-thread workgroup per batch, the records found by
+// the speculative parallel walk of specwalk.h (record p is [p, p + |Length varint| +
+// Length), :736-737), every verified thread then parsing its own records (:738-878) from
+// the LDS window.  Results are identical to v2_index_kernel (kept as RDK_HIP_IDX_V1=1).
+struct V2Idx {
+  // the walk's record classification, as v2_index_kernel's Length walk decides it
+  __device__ __forceinline__ uint32_t classify(const spec::Win &W, uint32_t p,
+                                               uint32_t &next) const {
+    if (p == W.len) return spec::kDone;
+    int64_t L;
+    const uint32_t sz = idx_varint([&](uint32_t q) { return W.b(q); }, p, W.end, L);
+    if (!sz) return (W.end < W.len && p + 10u > W.end) ? spec::kCut : spec::kErr;
+    if (L < 0 || uint64_t(L) > uint64_t(W.len - p - sz)) return spec::kErr;
+    const uint32_t e = p + sz + uint32_t(L);
+    if (e > W.end) return spec::kCut;
+    next = e;
+    return spec::kOk;
+  }
+  // heuristic record-start test (never decides a result): a Length of at least 6 whose
+  // record ends inside the batch, Attributes 0 (the writer's, rdkafka_msgset_writer.c:722),
+  // TimestampDelta and OffsetDelta varints, and the record after it looking the same with
+  // a larger OffsetDelta
+  __device__ __forceinline__ bool head(const spec::Win &W, uint32_t q, uint32_t &e,
+                                       int64_t &od) const {
+    auto g = [&](uint32_t x) { return W.b(x); };
+    int64_t L, tsd;
+    const uint32_t sz = idx_varint(g, q, q + 3u < W.end ? q + 3u : W.end, L);
+    if (!sz || L < 6 || uint64_t(L) > uint64_t(W.len - q - sz)) return false;
+    const uint32_t a = q + sz;
+    if (W.b(a) != 0u) return false;
+    const uint32_t n1 = idx_varint(g, a + 1u, W.end, tsd);
+    if (!n1) return false;
+    const uint32_t n2 = idx_varint(g, a + 1u + n1, W.end, od);
+    if (!n2 || od < 0) return false;
+    e = q + sz + uint32_t(L);
+    return true;
+  }
+  __device__ __forceinline__ bool plausible(const spec::Win &W, uint32_t q) const {
+    if (q + 24u > W.end) return false;
+    uint32_t e, e2;
+    int64_t od, od2;
+    if (!head(W, q, e, od)) return false;
+    if (e == W.len) return true;
+    if (e + 24u > W.end || !head(W, e, e2, od2)) return false;
+    return od2 > od && od2 - od < (int64_t(1) << 31);
+  }
+  // prefilter: byte q even and nonzero (the first byte of a positive zig-zag Length) and
+  // a zero byte (Attributes) at q+1 or q+2
+  __device__ __forceinline__ uint32_t scan(const spec::Win &W, uint32_t s0, uint32_t lim) const {
+    auto pre = [](const uint32_t *D, int k) {
+      return spec::nzb(D[k]) & spec::evb(D[k]) &
+             (spec::zb(__builtin_amdgcn_alignbyte(D[k + 1], D[k], 1u)) |
+              spec::zb(__builtin_amdgcn_alignbyte(D[k + 1], D[k], 2u)));
+    };
+    return spec::scan(W, s0, lim, pre, [&](uint32_t q) { return plausible(W, q); });
+  }
+};
+
+__global__ __launch_bounds__(spec::kThreads, 1) void v2_index_spec_kernel(
+    const uint8_t *__restrict__ hdr_base, const uint64_t *__restrict__ hdr_offs,
+    const uint8_t *__restrict__ rec_base, const uint64_t *__restrict__ rec_offs,
+    const uint32_t *__restrict__ rec_lens, const uint64_t *__restrict__ row_offs,
+    const uint32_t *__restrict__ row_caps, Rows rows, int32_t *__restrict__ count) {
+  __shared__ spec::Shared S;
+  __shared__ uint32_t big_s[2];
+  const uint32_t bi = blockIdx.x, t = threadIdx.x;
+  const uint8_t *hdr = hdr_base + hdr_offs[bi];
+  const int64_t base_off = ld_be64(hdr + 0);   // BaseOffset (msetr_v2_hdr, :742)
+  const int64_t base_ts = ld_be64(hdr + 27);   // BaseTimestamp (:911-912)
+  const uint8_t *rec = rec_base + rec_offs[bi];
+  const uint64_t row0 = row_offs[bi];
+  const uint32_t cap = row_caps[bi];
+  auto put = [&](uint32_t r, const IdxRow &o) {
+    const uint64_t row = row0 + r;
+    rows.offset[row] = base_off + o.od;        // :742
+    rows.timestamp[row] = base_ts + o.tsd;     // :911-912 (CreateTime)
+    rows.key_off[row] = o.ko;
+    rows.key_len[row] = o.kl;
+    rows.val_off[row] = o.vo;
+    rows.val_len[row] = o.vl;
+    rows.hdr_off[row] = o.ho;
+    rows.hdr_len[row] = o.hl;
+  };
+  auto emit = [&](const spec::Win &W, uint32_t c, uint32_t k, uint32_t rb) -> uint32_t {
+    auto g = [&](uint32_t q) { return W.b(q); };
+    uint32_t p = c;
+    for (uint32_t i = 0; i < k && rb + i < cap; ++i) {
+      IdxRow o;
+      uint32_t nx;
+      if (!idx_record(g, p, W.end, o, nx)) return rb + i;
+      put(rb + i, o);
+      p = nx;
+    }
+    return spec::kNone;
+  };
+  auto big = [&](const spec::Win &W, uint32_t base, uint32_t r, uint32_t &next) -> bool {
+    (void)W;
+    if (t == 0) {  // a record larger than the window: thread 0 from global memory
+      IdxRow o;
+      uint32_t nx = base;
+      const bool ok = idx_record([&](uint32_t q) -> uint32_t { return rec[q]; }, base,
+                                 rec_lens[bi], o, nx);
+      if (ok) put(r, o);
+      big_s[0] = ok;
+      big_s[1] = nx;
+    }
+    __syncthreads();
+    const bool ok = big_s[0] != 0;
+    next = big_s[1];
+    __syncthreads();
+    return ok;
+  };
+  const int32_t res = spec::walk(rec, rec_lens[bi], cap, S, V2Idx(), emit, big);
+  if (t == 0) count[bi] = res;
+}
+
 }  // namespace rdk
 
 using namespace rdk;
@@ -678,11 +795,19 @@ RDK_API int rdk_hip_msgset_v2_index(const void *d_hdr_base, const uint64_t *d_hd
     return set_error(RDK_HIP_E_INVAL, "null pointer");
   Rows r;
   std::memcpy(&r, rows, sizeof r);
-  hipLaunchKernelGGL(v2_index_kernel, dim3((n + kIdxWaves - 1) / kIdxWaves), dim3(64 * kIdxWaves),
-                     0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint8_t *>(d_hdr_base), d_hdr_offs,
-                     static_cast<const uint8_t *>(d_rec_base), d_rec_offs, d_rec_lens, d_row_offs,
-                     d_row_caps, r, d_count, n);
+  static const bool v1 = getenv("RDK_HIP_IDX_V1") && atoi(getenv("RDK_HIP_IDX_V1"));
+  if (v1)
+    hipLaunchKernelGGL(v2_index_kernel, dim3((n + kIdxWaves - 1) / kIdxWaves),
+                       dim3(64 * kIdxWaves), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const uint8_t *>(d_hdr_base), d_hdr_offs,
+                       static_cast<const uint8_t *>(d_rec_base), d_rec_offs, d_rec_lens,
+                       d_row_offs, d_row_caps, r, d_count, n);
+  else
+    hipLaunchKernelGGL(v2_index_spec_kernel, dim3(n), dim3(spec::kThreads), 0,
+                       static_cast<hipStream_t>(stream),
+                       static_cast<const uint8_t *>(d_hdr_base), d_hdr_offs,
+                       static_cast<const uint8_t *>(d_rec_base), d_rec_offs, d_rec_lens,
+                       d_row_offs, d_row_caps, r, d_count);
   RDK_HIP_CHECK(hipGetLastError());
   return RDK_HIP_OK;
 }

@@ -126,3 +126,22 @@ def test_v2_index_large_batches(engine, oracle_mod):
     cnt, host, r0 = _index(engine, bs)
     for i, b in enumerate(bs):
         _check_index(oracle_mod, b, cnt[i], host, r0[i])
+
+
+def test_v2_index_adversarial_payloads(engine, oracle_mod):
+    """Values that are themselves v2 record streams (or runs of 0x00 / 0x02 bytes): the
+    speculative segment guesses land inside values and must be rejected by the path check,
+    leaving rows identical to the oracle's."""
+    inner = oracle_mod.msgset_v2_write(W.gen_messages(300, seed=2), 0, 300)[61:]
+    vals = [inner, inner[:4000], bytes(700), b"\x02\x00" * 400, inner[17:9000]]
+    arena = np.frombuffer(b"".join(vals * 30), dtype=np.uint8)
+    n = len(vals) * 30
+    lens = np.array([len(v) for v in vals] * 30, dtype=np.int32)
+    m = {"arena": arena, "ts": np.arange(n, dtype=np.int64) * 3,
+         "key_off": np.zeros(n, dtype=np.uint64), "key_len": np.full(n, -1, dtype=np.int32),
+         "val_off": np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64),
+         "val_len": lens}
+    bs = [oracle_mod.msgset_v2_write(m, 0, n), oracle_mod.msgset_v2_write(m, 3, n - 3)]
+    cnt, host, r0 = _index(engine, bs)
+    for i, b in enumerate(bs):
+        _check_index(oracle_mod, b, cnt[i], host, r0[i])

@@ -57,6 +57,8 @@ def lib():
                                            C.c_size_t, C.c_int]
         L.or_xxh32.restype = C.c_uint32
         L.or_xxh32.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32]
+        L.or_lz4hc_compress_block.restype = C.c_int
+        L.or_lz4hc_compress_block.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
         L.or_lz4_compress_block.restype = C.c_int
         L.or_lz4_compress_block.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
         L.or_lz4_decompress_block.restype = C.c_int
@@ -115,6 +117,8 @@ def ref():
         R.ref_lz4_decompress_safe.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         R.ref_lz4_compress_block.restype = C.c_int
         R.ref_lz4_compress_block.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        R.ref_lz4hc_compress_block.restype = C.c_int
+        R.ref_lz4hc_compress_block.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
         R.ref_rdk_lz4_compress.restype = C.c_int
         R.ref_rdk_lz4_compress.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_char_p),
                                            C.POINTER(C.c_size_t), C.c_int,
@@ -167,6 +171,16 @@ def lz4_compress_block(data: bytes, acceleration: int = 1) -> bytes | None:
     src = _buf(data)
     dst = C.create_string_buffer(max(16, n + 16))
     r = lib().or_lz4_compress_block(src, n, dst, max(0, n - 1), acceleration)
+    return None if r == 0 else dst.raw[:r]
+
+
+def lz4hc_compress_block(data: bytes, level: int = 9) -> bytes | None:
+    """LZ4HC hash-chain block (levels 3..9, cap = n-1); None means 'stored raw'."""
+    n = len(data)
+    src = _buf(data)
+    dst = C.create_string_buffer(max(16, n + 16))
+    r = lib().or_lz4hc_compress_block(src, n, dst, max(0, n - 1), level)
+    assert r >= 0, "level not restated"
     return None if r == 0 else dst.raw[:r]
 
 
@@ -253,6 +267,15 @@ def ref_lz4_compress_block(data: bytes, acceleration: int = 1) -> bytes | None:
     src = _buf(data)
     dst = C.create_string_buffer(max(16, n + 16))
     r = R.ref_lz4_compress_block(src, n, dst, max(0, n - 1), acceleration)
+    return None if r == 0 else dst.raw[:r]
+
+
+def ref_lz4hc_compress_block(data: bytes, level: int = 9) -> bytes | None:
+    R = ref()
+    n = len(data)
+    src = _buf(data)
+    dst = C.create_string_buffer(max(16, n + 16))
+    r = R.ref_lz4hc_compress_block(src, n, dst, max(0, n - 1), level)
     return None if r == 0 else dst.raw[:r]
 
 

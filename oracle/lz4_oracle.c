@@ -378,9 +378,12 @@ static size_t frame_header(uint8_t *out) {
     return 7;
 }
 
-static size_t make_block(uint8_t *dst, const uint8_t *src, size_t n, int accel) {
-    /* LZ4F_makeBlock (lz4frame.c:739-761) */
-    int c = or_lz4_compress_block(src, (int)n, dst + 4, (int)n - 1, accel);
+static size_t make_block(uint8_t *dst, const uint8_t *src, size_t n, int level) {
+    /* LZ4F_makeBlock (lz4frame.c:739-761) with LZ4F_selectCompression
+     * (lz4frame.c:797-805): levels >= 3 take LZ4F_compressBlockHC */
+    int accel = level < 0 ? -level + 1 : 1;              /* lz4frame.c:766 */
+    int c = level >= 3 ? or_lz4hc_compress_block(src, (int)n, dst + 4, (int)n - 1, level)
+                       : or_lz4_compress_block(src, (int)n, dst + 4, (int)n - 1, accel);
     if (c == 0) {
         wr_le32(dst, (uint32_t)n | LZ4F_BLOCK_UNCOMPRESSED);
         memcpy(dst + 4, src, n);
@@ -419,8 +422,7 @@ static int fixup_framing(uint8_t *in, size_t inlen) {
 int or_rdk_lz4_compress(int proper_hc, int comp_level, const uint8_t *src,
                         size_t len, uint8_t **out, size_t *outlen) {
     *out = NULL;
-    if (comp_level >= 3) return OR_ERR__BAD_COMPRESSION; /* LZ4HC: not restated */
-    int accel = comp_level < 0 ? -comp_level + 1 : 1;    /* lz4frame.c:766 */
+    if (comp_level >= 10) return OR_ERR__BAD_COMPRESSION; /* LZ4HC optimal: not restated */
     size_t cap = or_lz4f_compress_bound(len);
     uint8_t *o = (uint8_t *)malloc(cap);
     if (!o) return OR_ERR__CRIT_SYS_RESOURCE;
@@ -429,7 +431,7 @@ int or_rdk_lz4_compress(int proper_hc, int comp_level, const uint8_t *src,
      * blocks plus one final partial block (lz4frame.c:883-893, 936-972). */
     for (size_t pos = 0; pos < len; pos += BLOCK64K) {
         size_t n = len - pos < BLOCK64K ? len - pos : BLOCK64K;
-        of += make_block(o + of, src + pos, n, accel);
+        of += make_block(o + of, src + pos, n, comp_level);
     }
     wr_le32(o + of, 0);                                  /* end mark */
     of += 4;

@@ -62,6 +62,13 @@ int or_lz4_compress_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap,
  * of dst (linked blocks).  Returns decoded size or a negative error. */
 int or_lz4_decompress_block(const uint8_t *src, int csize, uint8_t *dst,
                             int dst_cap, int dict_size);
+/* LZ4HC hash chain (lz4hc_oracle.c): LZ4HC_compress_hashChain (lz4hc.c:532-746)
+ * as LZ4F_compressBlockHC (lz4frame.c:782) reaches it for levels 3..9: fresh
+ * window per block, limitedOutput.  Returns the size, 0 if it does not fit,
+ * -1 for levels >= 10 (LZ4HC_compress_optimal, not restated). */
+int or_lz4hc_compress_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap, int level);
+/* nbSearches of clTable (lz4hc.c:775-789) for a hash-chain level */
+int or_lz4hc_attempts(int level);
 
 /* ---- LZ4F frame ---------------------------------------------------------- */
 /* Error codes returned by the rd_kafka_lz4_* restatements (rdkafka.h:258-268) */
@@ -71,7 +78,8 @@ int or_lz4_decompress_block(const uint8_t *src, int csize, uint8_t *dst,
 #define OR_ERR__CRIT_SYS_RESOURCE (-194)
 
 /* rd_kafka_lz4_compress (rdkafka_lz4.c:329-442) with the reference's prefs
- * {blockIndependent, comp_level}.  Levels >= 3 (LZ4HC) are not restated and
+ * {blockIndependent, comp_level}.  Levels 3..9 go through the LZ4HC hash
+ * chain (lz4hc_oracle.c); levels >= 10 (LZ4HC optimal) are not restated and
  * return OR_ERR__BAD_COMPRESSION.  *out is malloc()ed. */
 int or_rdk_lz4_compress(int proper_hc, int comp_level, const uint8_t *src,
                         size_t len, uint8_t **out, size_t *outlen);

@@ -17,6 +17,7 @@
 #define LZ4_STATIC_LINKING_ONLY
 #include "lz4.h"
 #include "lz4frame.h"
+#include "lz4hc.h"
 #include "xxhash.h"
 
 #define ERR_BAD_MSG (-199)
@@ -37,6 +38,14 @@ int ref_lz4_compress_block(const char *src, int n, char *dst, int cap, int accel
     LZ4_stream_t st;
     LZ4_initStream(&st, sizeof st);
     return LZ4_compress_fast_extState_fastReset(&st, src, dst, n, cap, accel);
+}
+
+/* One LZ4HC block as LZ4F_compressBlockHC reaches it (lz4frame.c:782-789):
+ * LZ4_compress_HC_extStateHC_fastReset, dstCapacity = srcSize-1. */
+int ref_lz4hc_compress_block(const char *src, int n, char *dst, int cap, int level) {
+    static __thread LZ4_streamHC_t st;
+    LZ4_initStreamHC(&st, sizeof st);
+    return LZ4_compress_HC_extStateHC_fastReset(&st, src, dst, n, cap, level);
 }
 
 static int break_framing(char *out, size_t outlen) {

@@ -13,6 +13,8 @@ Outputs (all data, no reference source):
                               the reference's rd_kafka_lz4_compress path makes
                               (vendored lz4 1.9.2 LZ4F), and of its payload.
   frame_*.lz4              -- the frames themselves for inputs <= 64 KiB.
+  lz4hc_frames.json        -- the same for compression.level 3..9 (LZ4HC hash
+                              chain, lz4frame.c:782 -> lz4hc.c:532-746).
   lz4f_decode_cases.json   -- deterministic malformed / edge-case frames and
                               the reference decoder's verdict (err, len,
                               sha256), exercising rdkafka_lz4.c:167-317.
@@ -101,6 +103,25 @@ def mutate_cases(frame: bytes, rnd: random.Random, count: int):
     return cases
 
 
+HC_INPUTS = ("json_s42_65536", "json_s42_65537", "json_s42_262144", "json_s7_13",
+             "json_s7_4096", "zeros_200000", "pattern_70000", "random_70000", "mixed_65536")
+
+
+def hc_frames() -> None:
+    """LZ4HC (levels 3..9) frames of the reference's rd_kafka_lz4_compress path."""
+    out = {}
+    for name in HC_INPUTS:
+        data = input_by_name(name)
+        for level in range(3, 10):
+            err, fr = O.ref_rdk_lz4_compress(data, comp_level=level)
+            assert err == 0
+            e2, payload, _ = O.ref_rdk_lz4_decompress(fr, max_msg_size=1 << 30)
+            assert e2 == 0 and payload == data
+            out[f"{name}@{level}"] = {"input": name, "level": level, "input_len": len(data),
+                                      "frame_len": len(fr), "frame_sha256": sha(fr)}
+    json.dump(out, open(os.path.join(HERE, "lz4hc_frames.json"), "w"), indent=1)
+
+
 def main() -> None:
     O.build(ref=True)
     assert O.ref_available(), "oracle/_ref/libreflz4.so not built"
@@ -134,6 +155,7 @@ def main() -> None:
             rec["frame_file"] = fn
         frames[name] = rec
     json.dump(frames, open(os.path.join(HERE, "lz4f_frames.json"), "w"), indent=1)
+    hc_frames()
 
     # ---- decoder verdicts on malformed / edge frames
     rnd = random.Random(77)
@@ -212,4 +234,8 @@ def apply_edit(frame: bytes, edit: dict) -> bytes:
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--hc-only"]:
+        O.build(ref=True)
+        hc_frames()
+    else:
+        main()

@@ -372,6 +372,9 @@ int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
                               const uint32_t *d_in_lens, uint8_t *d_out,
                               const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
                               hipStream_t s);
+int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
+                          uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                          uint32_t n, int level, hipStream_t s);
 
 }  // namespace rdk
 
@@ -386,10 +389,14 @@ RDK_API int rdk_hip_lz4f_compress(const void *d_in, const uint64_t *d_in_offs,
   Ctx *c = ctx();
   if (!c) return RDK_HIP_E_NODEV;
   if (!n) return RDK_HIP_OK;
-  if (level >= 3) return set_error(RDK_HIP_E_INVAL, "LZ4HC levels (>=3) are not implemented");
+  if (level >= 10)
+    return set_error(RDK_HIP_E_INVAL, "LZ4HC optimal levels (>=10) are not implemented");
   if (!d_in || !d_in_offs || !d_in_lens || !d_out || !d_out_offs || !d_out_lens)
     return set_error(RDK_HIP_E_INVAL, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (level >= 3)  // LZ4F_selectCompression (lz4frame.c:797-805): LZ4HC hash chain
+    return lz4hc_compress_device(static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
+                                 static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n, level, s);
   const int accel = level < 0 ? -level + 1 : 1;  // LZ4F_compressBlock, lz4frame.c:766
   return lz4f_compress_device(c, static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
                               static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n, accel, s);

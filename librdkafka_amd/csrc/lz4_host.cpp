@@ -15,6 +15,9 @@
 
 namespace rdk {
 
+int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
+                          uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                          uint32_t n, int level, hipStream_t s);
 int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
                          const uint32_t *d_in_lens, uint8_t *d_out, const uint64_t *d_out_offs,
                          uint32_t *d_out_lens, uint32_t n, int accel, hipStream_t s);
@@ -87,8 +90,13 @@ int lz4f_compress_host(Ctx *c, size_t len, int proper_hc, int level, void **out,
   if (len) RDK_HIP_CHECK(hipMemcpyAsync(d_in, c->h_stage, len, hipMemcpyHostToDevice, c->stream));
   RDK_HIP_CHECK(hipMemcpyAsync(dd, hd, 24, hipMemcpyHostToDevice, c->stream));
   const int accel = level < 0 ? -level + 1 : 1;
-  if ((rc = lz4f_compress_device(c, d_in, dd, d_len, d_out, dd + 1, d_olen, 1, accel, c->stream)))
+  if (level >= 3) {  // LZ4F_selectCompression (lz4frame.c:797-805): LZ4HC hash chain
+    if ((rc = lz4hc_compress_device(d_in, dd, d_len, d_out, dd + 1, d_olen, 1, level, c->stream)))
+      return rc;
+  } else if ((rc = lz4f_compress_device(c, d_in, dd, d_len, d_out, dd + 1, d_olen, 1, accel,
+                                        c->stream))) {
     return rc;
+  }
   RDK_HIP_CHECK(hipMemcpyAsync(c->h_desc + 32, d_olen, 4, hipMemcpyDeviceToHost, c->stream));
   RDK_HIP_CHECK(hipStreamSynchronize(c->stream));
   uint32_t flen;

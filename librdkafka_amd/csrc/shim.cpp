@@ -95,9 +95,9 @@ RDK_API rd_kafka_resp_err_t rd_kafka_lz4_compress(rd_kafka_broker_t *rkb, int pr
                                                   int comp_level, rd_slice_t *slice,
                                                   void **outbuf, size_t *outlenp) {
   *outbuf = nullptr;
-  if (comp_level >= 3) {
-    // LZ4HC (lz4frame.c:797-805) is not implemented by the engine: hand the
-    // call to the next definition (librdkafka's own) if there is one.
+  if (comp_level >= 10) {
+    // LZ4HC optimal (lz4hc.c:1278, levels 10..12) is not implemented by the
+    // engine: hand the call to the next definition (librdkafka's own) if any.
     lz4c_fn next = reinterpret_cast<lz4c_fn>(dlsym(RTLD_NEXT, "rd_kafka_lz4_compress"));
     if (next && next != &rd_kafka_lz4_compress)
       return next(rkb, proper_hc, comp_level, slice, outbuf, outlenp);

@@ -53,7 +53,7 @@ def test_dropin_compress_segments_levels_legacy(engine, oracle_mod):
             oracle_mod.rdk_lz4_compress(data, comp_level=level)[1], level
     assert engine.rd_kafka_lz4_compress(0, 0, data)[1] == \
         oracle_mod.rdk_lz4_compress(data, proper_hc=0)[1]     # broken HC for MsgVersion 0
-    err, _ = engine.rd_kafka_lz4_compress(1, 9, data)         # LZ4HC, no next definition
+    err, _ = engine.rd_kafka_lz4_compress(1, 10, data)        # LZ4HC optimal, no next definition
     assert err == engine.RESP_ERR__BAD_COMPRESSION
 
 

@@ -154,7 +154,7 @@ def json_batches(n, size=JSON_BATCH, seed=42):
     return buf, offs, lens
 
 
-def bench_lz4c(args, rank, world, n=None, fast=False):
+def bench_lz4c(args, rank, world, n=None, fast=False, level=0):
     """configs[2]: LZ4F compress (rd_kafka_lz4_compress semantics) of 1 MiB
     JSON batches.  fast=False: frames byte-identical to the reference's;
     fast=True: the throughput-mode encoder (reference-decodable frames, ratio
@@ -167,7 +167,10 @@ def bench_lz4c(args, rank, world, n=None, fast=False):
     dst = torch.empty(n * bound + 256, dtype=torch.uint8, device="cuda")
     ooffs = torch.arange(n, dtype=torch.int64, device="cuda") * bound
     olens = torch.zeros(n, dtype=torch.int32, device="cuda")
-    comp = L.lz4f_compress_fast_batch if fast else L.lz4f_compress_batch
+    if fast:
+        comp = L.lz4f_compress_fast_batch
+    else:
+        comp = lambda *a: L.lz4f_compress_batch(*a, level=level)  # noqa: E731
     ms, kms = _timed(lambda: comp(src, offs, lens, dst, ooffs, olens),
                      args.steps, args.warmup, world)
     clen = int(olens.sum())
@@ -540,7 +543,7 @@ def cpu_baseline_crc(buf, n, size, seconds=8.0):
                       f", {cpu_model()}"}
 
 
-def cpu_baseline_lz4(kind, n=64, seconds=4.0):
+def cpu_baseline_lz4(kind, n=64, seconds=4.0, level=0):
     """Oracle restatement of rd_kafka_lz4_compress / _decompress (the
     reference's lz4 1.9.2 LZ4F path, byte-identical output) on CPU_THREADS
     host threads over n x 1 MiB JSON batches."""
@@ -556,9 +559,9 @@ def cpu_baseline_lz4(kind, n=64, seconds=4.0):
     coffs = (np.arange(n, dtype=np.uint64) * bound).astype(np.uint64)
     clens = np.zeros(n, dtype=np.uint32)
     lib = oracle.lib()
-    comp = lambda: lib.or_lz4f_compress_batches_mt(  # noqa: E731
+    comp = lambda: lib.or_lz4f_compress_batches_level_mt(  # noqa: E731
         src.ctypes.data, offs.ctypes.data, lens.ctypes.data, n, cbuf.ctypes.data,
-        coffs.ctypes.data, clens.ctypes.data, CPU_THREADS)
+        coffs.ctypes.data, clens.ctypes.data, level, CPU_THREADS)
     comp()
     dbuf = np.zeros(n * JSON_BATCH, dtype=np.uint8)
     dlens = np.zeros(n, dtype=np.uint32)
@@ -575,7 +578,8 @@ def cpu_baseline_lz4(kind, n=64, seconds=4.0):
             break
     return {"value": round(passes * n * JSON_BATCH / el / 1e9, 3), "unit": "GB/s",
             "cores": CPU_THREADS, "kind": "port",
-            "sample": f"{n} x 1 MiB JSON batches, {passes} passes, rd_kafka_lz4_{kind} restated, "
+            "sample": f"{n} x 1 MiB JSON batches, {passes} passes, rd_kafka_lz4_{kind} restated"
+                      f"{f' at compression.level {level}' if level else ''}, "
                       f"{cpu_model()}"}
 
 
@@ -648,12 +652,13 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="crc",
-                    choices=["crc", "lz4c", "lz4c_fast", "consumer", "producer", "serialize",
+                    choices=["crc", "lz4c", "lz4c_fast", "lz4hc", "consumer", "producer", "serialize",
                              "index", "legacy"])
     ap.add_argument("--batches", type=int, default=CRC_BATCHES)
     ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true")
+    ap.add_argument("--level", type=int, default=9, help="compression.level of --workload lz4hc")
     args = ap.parse_args()
 
     rank, local_rank, world = dist_env()
@@ -668,7 +673,9 @@ def main():
     L.init(local_rank)
 
     if args.workload != "crc":
-        if args.workload.startswith("lz4c"):
+        if args.workload == "lz4hc":
+            res = bench_lz4c(args, rank, world, level=args.level)
+        elif args.workload.startswith("lz4c"):
             res = bench_lz4c(args, rank, world, fast=args.workload == "lz4c_fast")
         elif args.workload == "producer":
             res = bench_producer(args, rank, world)
@@ -692,7 +699,8 @@ def main():
                     cpu = cpu_baseline_legacy(*res["host_sample"])
                 else:
                     cpu = cpu_baseline_lz4("decompress" if args.workload == "consumer"
-                                           else "compress")
+                                           else "compress",
+                                           level=args.level if args.workload == "lz4hc" else 0)
             res.pop("host_sample", None)
             res["ms"] = t_max
             print(json.dumps({"workload": args.workload, "n_gpus": world, "steps": args.steps,
@@ -752,6 +760,11 @@ def main():
                                                     cpu("compress")),
                 "lz4f_compress_fast_1MiB_json": leg_line(
                     "lz4c_fast", bench_lz4c(sub, rank, world, fast=True), 3, 1, cpu("compress")),
+                # LZ4HC at its default level (LZ4HC_CLEVEL_DEFAULT = 9), 256 x 1 MiB
+                "lz4hc_compress_level9_1MiB_json": leg_line(
+                    "lz4hc", bench_lz4c(argparse.Namespace(steps=3, warmup=1, partitions=256),
+                                        rank, world, level=9), 3, 1,
+                    None if args.no_cpu_baseline else cpu_baseline_lz4("compress", level=9)),
                 "consumer_crc_verify_lz4f_decompress_1MiB": leg_line(
                     "consumer", bench_consumer(argparse.Namespace(steps=3, warmup=1, partitions=1024),
                                                rank, world), 3, 1, cpu("decompress")),

@@ -47,7 +47,7 @@ constexpr uint32_t kHcNone = 0xFFFFFFFFu;
 constexpr int kHcOptimalML = 18;             // lz4hc.c:74
 constexpr size_t kHcTab = size_t(4) << kHcHashLog;  // head / bucket start, u32
 constexpr size_t kHcScratch = kHcTab + 3 * 65536 * 2;  // + chain, rank, sorted (u16)
-constexpr unsigned kHcGrid = 2048;
+constexpr unsigned kHcGrid = 4096;  // 16 waves per CU (the kernel fits 20)
 
 struct HcBlock {
   uintptr_t s;       // block bytes (global)
@@ -419,7 +419,8 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n) {
 __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
-    const uint64_t *__restrict__ out_offs, uint32_t n, int attempts, uint8_t *scratch) {
+    const uint64_t *__restrict__ out_offs, uint32_t n, int attempts, uint8_t *scratch,
+    uint32_t *__restrict__ next_item) {
   HcBlock b;
   b.lane = threadIdx.x;
   uint8_t *sc = scratch + size_t(blockIdx.x) * kHcScratch;
@@ -429,9 +430,17 @@ __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
   b.sorted = b.rank + 65536;
   b.attempts = attempts;
   b.pa = attempts > 128;  // lz4hc.c:544
-  const uint64_t items = uint64_t(n) * kHcItems;
-  for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
-    const uint32_t f = uint32_t(it / kHcItems), kk = uint32_t(it % kHcItems);
+  // Work queue over (block slot, frame) items, slot-major: every wave takes
+  // the next item when it finishes one, so the parse's uneven cost per block
+  // spreads over the whole grid; the empty slots of short frames come last
+  // and cost one atomic each.
+  const uint32_t items = n * uint32_t(kHcItems);
+  for (;;) {
+    uint32_t it = 0;
+    if (b.lane == 0) it = atomicAdd(next_item, 1u);
+    it = uni(it);
+    if (it >= items) break;
+    const uint32_t f = it % n, kk = it / n;
     const uint32_t len = uni(in_lens[f]);
     const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
     for (uint32_t k = kk; k < nb; k += kHcItems) {
@@ -470,14 +479,17 @@ int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const 
   if (tl_hc.device != dev || !tl_hc.p) {
     if (tl_hc.p && tl_hc.device == dev) (void)hipFree(tl_hc.p);
     tl_hc.p = nullptr;
-    RDK_HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&tl_hc.p), kHcScratch * kHcGrid));
+    RDK_HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&tl_hc.p), kHcScratch * kHcGrid + 256));
     tl_hc.device = dev;
   }
+  if (n > (0xFFFFFFFFu / kHcItems) - kHcGrid) return RDK_HIP_RESP_ERR__BAD_COMPRESSION;
   const uint64_t items = uint64_t(n) * kHcItems;
   const unsigned grid = unsigned(items < kHcGrid ? items : kHcGrid);
   const int attempts = 1 << (level - 1);  // clTable rows 3..9: 4 .. 256
+  uint32_t *next_item = reinterpret_cast<uint32_t *>(tl_hc.p + kHcScratch * kHcGrid);
+  RDK_HIP_CHECK(hipMemsetAsync(next_item, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(lz4hc_compress_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
-                     d_in_lens, d_out, d_out_offs, n, attempts, tl_hc.p);
+                     d_in_lens, d_out, d_out_offs, n, attempts, tl_hc.p, next_item);
   lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;

@@ -75,6 +75,10 @@ def lib():
         L.or_lz4f_compress_batches_mt.restype = C.c_int
         L.or_lz4f_compress_batches_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.or_lz4f_compress_batches_level_mt.restype = C.c_int
+        L.or_lz4f_compress_batches_level_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p,
+                                                        C.c_size_t, C.c_void_p, C.c_void_p,
+                                                        C.c_void_p, C.c_int, C.c_int]
         L.or_lz4f_decompress_batches_mt.restype = C.c_int
         L.or_lz4f_decompress_batches_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -565,7 +565,7 @@ out:
 struct fjob {
     const uint8_t *base; const uint64_t *offs; const uint32_t *lens; size_t lo, hi;
     uint8_t *out; const uint64_t *out_offs; const uint32_t *out_caps; uint32_t *out_lens;
-    int decompress; int rc;
+    int decompress; int rc; int level;
 };
 
 static void *fworker(void *arg) {
@@ -578,7 +578,7 @@ static void *fworker(void *arg) {
             if (!e && rl <= j->out_caps[i]) memcpy(j->out + j->out_offs[i], r, rl);
             else if (!e) e = -1;
         } else {
-            e = or_rdk_lz4_compress(1, 0, j->base + j->offs[i], j->lens[i], &r, &rl);
+            e = or_rdk_lz4_compress(1, j->level, j->base + j->offs[i], j->lens[i], &r, &rl);
             if (!e) memcpy(j->out + j->out_offs[i], r, rl);
         }
         free(r);
@@ -590,7 +590,8 @@ static void *fworker(void *arg) {
 
 static int run_frames(const uint8_t *base, const uint64_t *offs, const uint32_t *lens,
                       size_t n, uint8_t *out, const uint64_t *out_offs,
-                      const uint32_t *caps, uint32_t *out_lens, int threads, int dec) {
+                      const uint32_t *caps, uint32_t *out_lens, int threads, int dec,
+                      int level) {
     if (threads < 1) threads = 1;
     if (threads > 512) threads = 512;
     pthread_t th[512];
@@ -598,7 +599,7 @@ static int run_frames(const uint8_t *base, const uint64_t *offs, const uint32_t 
     int rc = 0;
     for (int t = 0; t < threads; t++) {
         jobs[t] = (struct fjob){base, offs, lens, n * t / threads, n * (t + 1) / threads,
-                                out, out_offs, caps, out_lens, dec, 0};
+                                out, out_offs, caps, out_lens, dec, 0, level};
         pthread_create(&th[t], NULL, fworker, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) { pthread_join(th[t], NULL); if (jobs[t].rc) rc = jobs[t].rc; }
@@ -608,12 +609,19 @@ static int run_frames(const uint8_t *base, const uint64_t *offs, const uint32_t 
 int or_lz4f_compress_batches_mt(const uint8_t *base, const uint64_t *offs,
                                 const uint32_t *lens, size_t n, uint8_t *out,
                                 const uint64_t *out_offs, uint32_t *out_lens, int threads) {
-    return run_frames(base, offs, lens, n, out, out_offs, NULL, out_lens, threads, 0);
+    return run_frames(base, offs, lens, n, out, out_offs, NULL, out_lens, threads, 0, 0);
+}
+
+int or_lz4f_compress_batches_level_mt(const uint8_t *base, const uint64_t *offs,
+                                      const uint32_t *lens, size_t n, uint8_t *out,
+                                      const uint64_t *out_offs, uint32_t *out_lens,
+                                      int level, int threads) {
+    return run_frames(base, offs, lens, n, out, out_offs, NULL, out_lens, threads, 0, level);
 }
 
 int or_lz4f_decompress_batches_mt(const uint8_t *base, const uint64_t *offs,
                                   const uint32_t *lens, size_t n, uint8_t *out,
                                   const uint64_t *out_offs, const uint32_t *out_caps,
                                   uint32_t *out_lens, int threads) {
-    return run_frames(base, offs, lens, n, out, out_offs, out_caps, out_lens, threads, 1);
+    return run_frames(base, offs, lens, n, out, out_offs, out_caps, out_lens, threads, 1, 0);
 }

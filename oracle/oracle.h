@@ -98,6 +98,11 @@ int or_lz4f_compress_batches_mt(const uint8_t *base, const uint64_t *offs,
                                 const uint32_t *lens, size_t n,
                                 uint8_t *out, const uint64_t *out_offs,
                                 uint32_t *out_lens, int threads);
+/* Same at compression.level `level` (3..9: the LZ4HC hash chain). */
+int or_lz4f_compress_batches_level_mt(const uint8_t *base, const uint64_t *offs,
+                                      const uint32_t *lens, size_t n,
+                                      uint8_t *out, const uint64_t *out_offs,
+                                      uint32_t *out_lens, int level, int threads);
 int or_lz4f_decompress_batches_mt(const uint8_t *base, const uint64_t *offs,
                                   const uint32_t *lens, size_t n,
                                   uint8_t *out, const uint64_t *out_offs,

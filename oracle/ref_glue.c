@@ -15,6 +15,7 @@
 #include <string.h>
 
 #define LZ4_STATIC_LINKING_ONLY
+#define LZ4_HC_STATIC_LINKING_ONLY
 #include "lz4.h"
 #include "lz4frame.h"
 #include "lz4hc.h"

@@ -46,7 +46,7 @@ constexpr int kHcHashLog = 15;               // lz4hc.h:196
 constexpr uint32_t kHcNone = 0xFFFFFFFFu;
 constexpr int kHcOptimalML = 18;             // lz4hc.c:74
 constexpr size_t kHcTab = size_t(4) << kHcHashLog;  // head / bucket start, u32
-constexpr size_t kHcScratch = kHcTab + 3 * 65536 * 2;  // + chain, rank, sorted (u16)
+constexpr size_t kHcScratch = kHcTab + 3 * 65536 * 2 + 65536 * 4;  // + chain, rank, sorted (u16), tr (u32)
 constexpr unsigned kHcGrid = 4096;  // 16 waves per CU (the kernel fits 20)
 
 struct HcBlock {
@@ -55,6 +55,7 @@ struct HcBlock {
   uint16_t *chain;   // DELTANEXTU16 per position
   uint16_t *rank;    // index of the position inside its hash bucket
   uint16_t *sorted;  // positions ordered by (hash, position)
+  uint32_t *tr;      // per position: its index in sorted | its rank << 16
   int attempts;      // nbSearches
   int pa;            // patternAnalysis (levels 9+)
   int lane;
@@ -64,9 +65,37 @@ __device__ __forceinline__ uint32_t hc_hash(uint32_t v) {  // HASH_FUNCTION, lz4
   return (v * 2654435761u) >> (32 - kHcHashLog);
 }
 
-// LZ4_count by one lane: equal bytes from a / b, a never reaching lim
+// 16 bytes at any byte address through five aligned dword loads issued
+// together; touches at most the dword holding byte a+16 (callers keep a+32 <=
+// matchlimit = iend - LASTLITERALS, so nothing past the input is read)
+__device__ __forceinline__ void hc_ld16(uintptr_t a, uint32_t w[4]) {
+  const uintptr_t b = a & ~uintptr_t(3);
+  const uint32_t sh = uint32_t(a & 3u);
+  uint32_t d[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) d[j] = *(g_cu32 *)(b + 4 * j);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+}
+
+// LZ4_count by one lane: equal bytes from a / b, a never reaching lim.
+// 32 bytes per dependent round trip while they fit, then dwords, then bytes.
 __device__ __forceinline__ int hc_count(uintptr_t s, int a, int b, int lim) {
   const int a0 = a;
+  while (a + 32 <= lim) {
+    uint32_t x[8], y[8];
+    hc_ld16(s + a, x);
+    hc_ld16(s + a + 16, x + 4);
+    hc_ld16(s + b, y);
+    hc_ld16(s + b + 16, y + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t d = x[j] ^ y[j];
+      if (d) return a + 4 * j + (__builtin_ctz(d) >> 3) - a0;
+    }
+    a += 32;
+    b += 32;
+  }
   while (a + 4 <= lim) {
     const uint32_t x = ld32u(s + a) ^ ld32u(s + b);
     if (x) return a + (__builtin_ctz(x) >> 3) - a0;
@@ -177,7 +206,9 @@ __device__ void hc_build(const HcBlock &b, int npos) {
   __threadfence_block();
   for (int p = lane; p < npos; p += 64) {
     const uint32_t h = hc_hash(ld32u(b.s + p));
-    b.sorted[b.head[h] + b.rank[p]] = uint16_t(p);
+    const uint32_t r = b.rank[p], idx = b.head[h] + r;
+    b.sorted[idx] = uint16_t(p);
+    b.tr[p] = idx | (r << 16);
   }
   __threadfence_block();
 }
@@ -251,8 +282,9 @@ __device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int long
   if (b.pa && ((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24)))
     return hc_search_serial(b, ip, ilow, ihigh, longest, mpos, spos, pat);
   const int br = ip - ilow;
-  const int r = b.rank[ip];
-  const int top = int(b.head[hc_hash(pat)]) + r - 1;  // sorted[top] = latest earlier same-hash
+  const uint32_t t = b.tr[ip];  // one load instead of rank -> hash -> bucket start
+  const int r = int(t >> 16);
+  const int top = int(t & 0xFFFFu) - 1;  // sorted[top] = latest earlier same-hash
   const int total = r < b.attempts ? r : b.attempts;
   for (int c0 = 0; c0 < total; c0 += 64) {
     const int j = c0 + lane;
@@ -328,14 +360,61 @@ __device__ int hc_encode(const HcBlock &b, uintptr_t d, int &op, int oend, int &
   return 0;
 }
 
+// Whether the main loop's search at p (longest = MINMATCH-1) certainly finds
+// nothing: none of its first min(rank, attempts) chain candidates repeats the
+// 4 bytes at p (the only way such a search can succeed; lz4hc.c:264-266).
+// Positions it cannot settle cheaply (long buckets, level-9 repetitive
+// patterns) report false and get the full search.
+__device__ __forceinline__ bool hc_sure_miss(const HcBlock &b, int p, int mflimit) {
+  if (p > mflimit) return false;
+  const uint32_t pat = ld32u(b.s + p);
+  if (b.pa && ((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24))) return false;
+  const uint32_t t = b.tr[p];
+  const int r = int(t >> 16);
+  const int total = r < b.attempts ? r : b.attempts;
+  if (total == 0) return true;
+  if (total > 8) return false;
+  const int top = int(t & 0xFFFFu) - 1;
+  int c[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = j < total ? int(b.sorted[top - j]) : -1;
+  bool miss = true;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (c[j] >= 0 && ld32u(b.s + c[j]) == pat) miss = false;
+  return miss;
+}
+
 // LZ4HC_compress_hashChain (lz4hc.c:532-746).  Returns the compressed size or
 // 0 when the block does not fit in n-1 bytes.  n >= 13.
 __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n) {
   const int mflimit = n - kLz4MFLimit, matchlimit = n - kLz4LastLiterals, oend = n - 1;
+#ifdef RDK_HC_PROF
+  const uint64_t t0 = wall_clock64();
+#endif
   hc_build(b, mflimit + 1);
+#ifdef RDK_HC_PROF
+  const uint64_t t1 = wall_clock64();
+  int nskip = 0;
+#endif
   int ip = 0, anchor = 0, op = 0, unused = 0;
   int ml, ml0, ml2, ml3, start0, ref0, ref = 0, start2 = 0, ref2 = 0, start3 = 0, ref3 = 0;
+  int wbase = 0, wend = 0;  // positions [wbase, wend) have a sure-miss bit in wmiss
+  uint64_t wmiss = 0;
   while (ip <= mflimit) {
+    if (ip >= wend) {  // 64 positions settled in parallel, one per lane
+      wbase = ip;
+      wend = ip + 64;
+      wmiss = ballot(hc_sure_miss(b, ip + b.lane, mflimit));
+    }
+    const uint64_t run = ~(wmiss >> (ip - wbase));
+    if (!(run & 1u)) {  // the reference steps ip++ over each of these (lz4hc.c:568)
+#ifdef RDK_HC_PROF
+      nskip += run ? __builtin_ctzll(run) : wend - ip;
+#endif
+      ip += run ? __builtin_ctzll(run) : wend - ip;
+      continue;
+    }
     ml = hc_search(b, ip, ip, matchlimit, kLz4MinMatch - 1, ref, unused);
     if (ml < kLz4MinMatch) { ip++; continue; }
     start0 = ip; ref0 = ref; ml0 = ml;
@@ -413,6 +492,11 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n) {
     hc_copy(dst + op, b.s + anchor, run, b.lane);
     op += run;
   }
+#ifdef RDK_HC_PROF
+  if (b.lane == 0 && blockIdx.x < 4)
+    printf("HCPROF blk %d n %d build_us %.1f parse_us %.1f skipped %d out %d\n", int(blockIdx.x), n,
+           double(t1 - t0) / 100.0, double(wall_clock64() - t1) / 100.0, nskip, op);
+#endif
   return op;
 }
 
@@ -428,6 +512,7 @@ __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
   b.chain = reinterpret_cast<uint16_t *>(sc + kHcTab);
   b.rank = b.chain + 65536;
   b.sorted = b.rank + 65536;
+  b.tr = reinterpret_cast<uint32_t *>(b.sorted + 65536);
   b.attempts = attempts;
   b.pa = attempts > 128;  // lz4hc.c:544
   // Work queue over (block slot, frame) items, slot-major: every wave takes

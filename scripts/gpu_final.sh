@@ -13,6 +13,6 @@ cat "$O/bench.log"
 cd /tmp && export TMPDIR=/tmp
 P="$O/prof"; mkdir -p "$P"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$P/crc" -o k -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-legs > "$P/crc.log" 2>&1 || { echo TRACE1_FAILED; tail -20 "$P/crc.log"; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$P/lz4hc" -o k -- python3 $R/bench.py --workload lz4hc --level 9 --partitions 64 --steps 3 --warmup 1 --no-cpu-baseline > "$P/lz4hc.log" 2>&1 || { echo TRACE2_FAILED; tail -20 "$P/lz4hc.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$P/lz4hc" -o k -- python3 $R/bench.py --workload lz4hc --level 9 --partitions 256 --steps 3 --warmup 1 --no-cpu-baseline > "$P/lz4hc.log" 2>&1 || { echo TRACE2_FAILED; tail -20 "$P/lz4hc.log"; exit 1; }
 for d in crc lz4hc; do echo "== $d"; grep -h "GB" "$P/$d.log" | cut -c1-300; head -4 "$P/$d/k_kernel_stats.csv"; done
 echo ALL_OK

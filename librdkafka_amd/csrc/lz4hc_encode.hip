@@ -153,10 +153,15 @@ __device__ void hc_build(const HcBlock &b, int npos) {
   __threadfence_block();
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+  // the next step's source word is loaded during this step (it does not
+  // depend on the head[] updates), leaving one dependent round trip per step
+  uint32_t w_next = lane < npos ? ld32u(b.s + lane) : 0u;
   for (int base = 0; base < npos; base += 64) {
     const int p = base + lane;
     const bool valid = p < npos;
-    const uint32_t h = valid ? hc_hash(ld32u(b.s + p)) : 0u;
+    const uint32_t h = valid ? hc_hash(w_next) : 0u;
+    w_next = p + 64 < npos ? ld32u(b.s + p + 64) : 0u;
+    if (valid) b.tr[p] = h;  // the scatter below reads the hash back from here
     uint64_t eq = ballot(valid);
 #pragma unroll
     for (int bit = 0; bit < kHcHashLog; ++bit) {
@@ -204,11 +209,26 @@ __device__ void hc_build(const HcBlock &b, int npos) {
     }
   }
   __threadfence_block();
-  for (int p = lane; p < npos; p += 64) {
-    const uint32_t h = hc_hash(ld32u(b.s + p));
-    const uint32_t r = b.rank[p], idx = b.head[h] + r;
-    b.sorted[idx] = uint16_t(p);
-    b.tr[p] = idx | (r << 16);
+  // scatter, four steps' loads issued before their stores
+  for (int p0 = lane; p0 < npos; p0 += 256) {
+    uint32_t h[4], r[4], st[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = p0 + 64 * j;
+      h[j] = p < npos ? b.tr[p] : 0u;
+      r[j] = p < npos ? uint32_t(b.rank[p]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[j] = b.head[h[j]];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = p0 + 64 * j;
+      if (p < npos) {
+        const uint32_t idx = st[j] + r[j];
+        b.sorted[idx] = uint16_t(p);
+        b.tr[p] = idx | (r[j] << 16);
+      }
+    }
   }
   __threadfence_block();
 }

@@ -57,6 +57,19 @@ def barrier(world: int) -> None:
         dist.barrier()
 
 
+def launch_ranks(n: int) -> int:
+    """python -m torch.distributed.run, one rank per GPU on this node, same arguments."""
+    import socket
+    import subprocess
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    return subprocess.call(cmd + sys.argv[1:])
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -661,16 +674,25 @@ def main():
     ap.add_argument("--level", type=int, default=9, help="compression.level of --workload lz4hc")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # Started by hand with --gpus N: this parent never touches the GPU; it starts one
+        # rank per GPU the way the driver does and hands back the launcher's exit code.
+        sys.exit(launch_ranks(args.gpus))
     rank, local_rank, world = dist_env()
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: start it with "
+                 f"--nproc-per-node {args.gpus} (or without a launcher)")
     import torch
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local_rank)
+    # one rank per GPU; with fewer GPUs than ranks (a rehearsal on one device) ranks share
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     import librdkafka_amd as L
     if not os.path.exists(L.LIB_PATH):
-        L.build()
-    L.init(local_rank)
+        raise SystemExit(f"{L.LIB_PATH} is not built: run __graft_entry__.build()")
+    L.init(device)
 
     if args.workload != "crc":
         if args.workload == "lz4hc":

@@ -15,10 +15,18 @@
  *     stream.  Plain pointers and sizes only; `stream` is a hipStream_t
  *     passed as void* (NULL = the HIP null stream, as in the HIP API).
  *
- * Every function that touches the GPU fails loudly (returns RDK_HIP_E_* or,
- * for the drop-in symbols, which have no error channel, prints and aborts)
- * when no gfx950 device / code object is available.  There is no silent CPU
- * path; the only CPU work in the engine is frame-header bookkeeping.
+ * Every function that touches the GPU fails loudly when no gfx950 device /
+ * code object is available or a device call fails; there is no CPU path (the
+ * only CPU work in the engine is frame-header bookkeeping):
+ *   - rdk_hip_* return RDK_HIP_E_* and set rdk_hip_last_error();
+ *   - rd_kafka_lz4_compress / _decompress return the reference's own codes
+ *     (__CRIT_SYS_RESOURCE: no device or out of memory; __BAD_COMPRESSION: any
+ *     other device failure) and report the first failure on stderr, so the
+ *     writer sends the MessageSet uncompressed (rdkafka_msgset_writer.c:1175)
+ *     and the reader raises a consumer error (rdkafka_msgset_reader.c:517-526);
+ *   - crc32c / rd_slice_crc32c / rd_slice_crc32 return the checksum itself and
+ *     have no error channel: a failed device call is retried once, then the
+ *     process is aborted with a message rather than handed a wrong CRC.
  */
 #ifndef LIBRDKAFKA_HIP_H
 #define LIBRDKAFKA_HIP_H
@@ -67,11 +75,13 @@ uint32_t rd_slice_crc32(rd_slice_t *slice);
 
 /* Replaces rd_kafka_lz4_compress() (src/rdkafka_lz4.c:329-442).  LZ4F frame
  * with prefs {blockIndependent, comp_level}, 64 KB blocks; *outbuf is
- * malloc()ed (caller frees with free()); slice is consumed.  comp_level >= 3
- * (LZ4HC) is not implemented on the GPU: the call is forwarded to the next
- * definition of the symbol (librdkafka's own) when one is loaded, otherwise
- * __BAD_COMPRESSION is returned (the writer then sends uncompressed,
- * rdkafka_msgset_writer.c:1175). */
+ * malloc()ed (caller frees with free()); slice is consumed.  comp_level < 3
+ * runs LZ4_compress_generic's parse and 3..9 the LZ4HC hash-chain parse
+ * (lz4frame.c:797-805), both byte-identical to the reference's frames.
+ * comp_level >= 10 (LZ4HC optimal, lz4hc.c:1278) is not implemented:
+ * __BAD_COMPRESSION is returned and the writer sends the MessageSet
+ * uncompressed (rdkafka_msgset_writer.c:1175).  No call is ever forwarded to
+ * another definition of the symbol. */
 rd_kafka_resp_err_t rd_kafka_lz4_compress(rd_kafka_broker_t *rkb, int proper_hc,
                                           int comp_level, rd_slice_t *slice,
                                           void **outbuf, size_t *outlenp);
@@ -151,7 +161,8 @@ int rdk_hip_msgset_v2_crc(void *d_base, const uint64_t *d_batch_offs,
 /* LZ4F compression of n independent inputs (rd_kafka_lz4_compress semantics
  * per input, prefs {blockIndependent, level}).  Frame i is written to
  * d_out + d_out_offs[i] (capacity rdk_hip_lz4f_compress_bound(len)); its
- * size goes to d_out_lens[i].  `level` as compression.level (<3). */
+ * size goes to d_out_lens[i].  `level` as compression.level: < 3 the fast
+ * parse, 3..9 LZ4HC (byte-identical frames); >= 10 is RDK_HIP_E_INVAL. */
 size_t rdk_hip_lz4f_compress_bound(size_t len);
 int rdk_hip_lz4f_compress(const void *d_in, const uint64_t *d_in_offs,
                           const uint32_t *d_in_lens, void *d_out,

@@ -25,9 +25,15 @@ struct Ctx {
   // pinned host staging (grow-only)
   uint8_t *h_stage = nullptr;
   size_t h_cap = 0;
-  // device scratch (grow-only), two independent regions
-  uint8_t *d_stage[2] = {nullptr, nullptr};
-  size_t d_cap[2] = {0, 0};
+  // device scratch (grow-only), independent regions: kScratchStage is the drop-in
+  // symbols' staging (only ever used on `stream`, which every drop-in call leaves
+  // idle); kScratchDecode / kScratchHc / kScratchCrc hold the batch API's descriptors, the
+  // LZ4HC tables and the split CRC's partial registers and follow the caller's streams (scratch_acquire / _release)
+  uint8_t *d_stage[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t d_cap[4] = {0, 0, 0, 0};
+  hipStream_t d_last[4] = {nullptr, nullptr, nullptr, nullptr};  // stream of the last user
+  hipEvent_t d_done[4] = {nullptr, nullptr, nullptr, nullptr};  // recorded after the last use
+  bool d_used[4] = {false, false, false, false};
   // small device descriptor buffer
   uint8_t *d_desc = nullptr;
   size_t d_desc_cap = 0;
@@ -40,6 +46,13 @@ Ctx *ctx();
 int ensure_host(Ctx *c, size_t bytes);
 int ensure_dev(Ctx *c, int which, size_t bytes);
 int ensure_desc(Ctx *c, size_t bytes);
+constexpr int kScratchStage = 0, kScratchDecode = 1, kScratchHc = 2, kScratchCrc = 3;
+constexpr int kScratchRegions = 4;
+// Stream-ordered reuse of one scratch region by kernels on any stream: acquire makes
+// stream `s` wait for the region's previous user (an event, no host wait unless the
+// region has to grow), release marks the end of this use on `s`.
+int scratch_acquire(Ctx *c, int which, size_t bytes, hipStream_t s);
+int scratch_release(Ctx *c, int which, hipStream_t s);
 
 // Device-resident CRC tables for `device` (uploaded once per device).  kind selects the
 // polynomial: kCrcKind32C (CRC-32C, crc32c.c) or kCrcKind32 (CRC-32/zlib, rdcrc32.h).
@@ -50,7 +63,8 @@ const uint32_t *crc_tables_v4_dev(int device, int kind = kCrcKind32C);  // v4: 1
 // x^(2^k) mod P table (k = 0..63) for arbitrary-length shifts.
 const uint32_t *crc_x2n_dev(int device, int kind = kCrcKind32C);
 
-// Aborts the process with a message (drop-in symbols have no error channel).
+// Aborts the process with a message: only for the drop-in CRC symbols, whose
+// signatures have no error channel, after a retry.
 [[noreturn]] void fatal(const char *what);
 
 }  // namespace rdk
@@ -59,6 +73,8 @@ const uint32_t *crc_x2n_dev(int device, int kind = kCrcKind32C);
   do {                                                                        \
     hipError_t _e = (expr);                                                   \
     if (_e != hipSuccess)                                                     \
-      return ::rdk::set_error(-2, "%s failed: %s (%s:%d)", #expr,             \
+      return ::rdk::set_error(_e == hipErrorOutOfMemory ? RDK_HIP_E_NOMEM     \
+                                                        : RDK_HIP_E_HIP,      \
+                              "%s failed: %s (%s:%d)", #expr,                 \
                               hipGetErrorString(_e), __FILE__, __LINE__);     \
   } while (0)

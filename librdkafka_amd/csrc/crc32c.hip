@@ -924,28 +924,30 @@ static void launch_v2(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *
 }
 
 template <int MODE>
-static void launch_v2_any(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *caps,
-                          uint32_t *out, uint32_t n, hipStream_t s) {
+static int launch_v2_any(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_t *caps,
+                         uint32_t *out, uint32_t n, hipStream_t s) {
   // fewer than 2 batches per group slot of the chip: split every range into chunks
   constexpr uint32_t kSlots = 256u * kV4Groups;
   if (crc_variant() == 4 && n <= kSlots / 2) {
     const uint32_t nch = std::min(64u, kSlots / n);
-    uint32_t *raw = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void **>(&raw), size_t(n) * nch * 4, s) != hipSuccess) {
-      set_error(RDK_HIP_E_NOMEM, "split scratch");
-      return;
-    }
+    // at most kSlots partial registers (64 KiB): the thread's kScratchCrc region
+    int rc = scratch_acquire(c, kScratchCrc, size_t(kSlots) * 4, s);
+    if (rc) return rc;
+    uint32_t *raw = reinterpret_cast<uint32_t *>(c->d_stage[kScratchCrc]);
     const uint32_t items = n * nch;
     hipLaunchKernelGGL(crc32c_msgset_v2_split_kernel, dim3(crc_grid_v4(items)), dim3(kV4Block),
                        0, s, b, offs, caps, n, nch, raw, crc_tables_v4_dev(c->device));
     hipLaunchKernelGGL(crc32c_msgset_v2_combine_kernel<MODE>, dim3((n + 63) / 64), dim3(64), 0,
                        s, b, offs, caps, n, nch, raw, out, crc_x2n_dev(c->device));
-    (void)hipFreeAsync(raw, s);
+    RDK_HIP_CHECK(hipGetLastError());
+    return scratch_release(c, kScratchCrc, s);
   } else if (crc_variant() == 4)
     hipLaunchKernelGGL(crc32c_msgset_v2_v4_kernel<MODE>, dim3(crc_grid_v4(n)), dim3(kV4Block), 0,
                        s, b, offs, caps, out, n, crc_tables_v4_dev(c->device));
   else if (crc_variant() == 3) launch_v2<3, MODE>(c, b, offs, caps, out, n, s);
   else launch_v2<1, MODE>(c, b, offs, caps, out, n, s);
+  RDK_HIP_CHECK(hipGetLastError());
+  return RDK_HIP_OK;
 }
 
 }  // namespace rdk
@@ -976,17 +978,12 @@ RDK_API int rdk_hip_msgset_v2_crc(void *d_base, const uint64_t *d_batch_offs,
   uint8_t *b = static_cast<uint8_t *>(d_base);
   switch (mode) {
     case RDK_HIP_V2_CRC_COMPUTE:
-      launch_v2_any<RDK_HIP_V2_CRC_COMPUTE>(c, b, d_batch_offs, d_batch_caps, d_out, n, s);
-      break;
+      return launch_v2_any<RDK_HIP_V2_CRC_COMPUTE>(c, b, d_batch_offs, d_batch_caps, d_out, n, s);
     case RDK_HIP_V2_CRC_FINALIZE:
-      launch_v2_any<RDK_HIP_V2_CRC_FINALIZE>(c, b, d_batch_offs, d_batch_caps, d_out, n, s);
-      break;
+      return launch_v2_any<RDK_HIP_V2_CRC_FINALIZE>(c, b, d_batch_offs, d_batch_caps, d_out, n, s);
     case RDK_HIP_V2_CRC_VERIFY:
-      launch_v2_any<RDK_HIP_V2_CRC_VERIFY>(c, b, d_batch_offs, d_batch_caps, d_out, n, s);
-      break;
+      return launch_v2_any<RDK_HIP_V2_CRC_VERIFY>(c, b, d_batch_offs, d_batch_caps, d_out, n, s);
     default:
       return set_error(RDK_HIP_E_INVAL, "bad mode %d", mode);
   }
-  RDK_HIP_CHECK(hipGetLastError());
-  return RDK_HIP_OK;
 }

@@ -102,10 +102,13 @@ int bind(int dev) {
     RDK_HIP_CHECK(hipStreamCreateWithFlags(&tl_ctx->stream, hipStreamNonBlocking));
     tl_ctx->device = dev;
     // device scratch belongs to the old device: drop it
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kScratchRegions; ++i) {
       if (tl_ctx->d_stage[i]) (void)hipFree(tl_ctx->d_stage[i]);
       tl_ctx->d_stage[i] = nullptr;
       tl_ctx->d_cap[i] = 0;
+      tl_ctx->d_used[i] = false;
+      if (tl_ctx->d_done[i]) (void)hipEventDestroy(tl_ctx->d_done[i]);
+      tl_ctx->d_done[i] = nullptr;
     }
     if (tl_ctx->d_desc) (void)hipFree(tl_ctx->d_desc);
     tl_ctx->d_desc = nullptr;
@@ -142,29 +145,77 @@ int ensure_host(Ctx *c, size_t bytes) {
   return 0;
 }
 
+// Upper bound on any one device scratch region, from $RDK_HIP_MAX_SCRATCH_BYTES
+// (0 / unset = no bound): lets a deployment cap the engine's footprint and lets the
+// tests force the allocation-failure paths.
+static size_t scratch_limit() {
+  const char *e = getenv("RDK_HIP_MAX_SCRATCH_BYTES");
+  return e ? size_t(strtoull(e, nullptr, 10)) : 0;
+}
+
+static int dev_alloc(uint8_t **p, size_t n) {
+  const size_t lim = scratch_limit();
+  if (lim && n > lim)
+    return set_error(RDK_HIP_E_NOMEM, "device scratch of %zu bytes exceeds RDK_HIP_MAX_SCRATCH_BYTES=%zu",
+                     n, lim);
+  RDK_HIP_CHECK(hipMalloc(reinterpret_cast<void **>(p), n));
+  return 0;
+}
+
+// kScratchStage only: used on c->stream alone, and every drop-in call returns with
+// that stream idle, so growing needs no wait.
 int ensure_dev(Ctx *c, int which, size_t bytes) {
   if (c->d_cap[which] >= bytes) return 0;
-  if (c->d_stage[which]) {
-    // the buffer may be in flight on any stream the caller passed: drain all
-    (void)hipDeviceSynchronize();
-    (void)hipFree(c->d_stage[which]);
-  }
+  if (c->d_stage[which]) (void)hipFree(c->d_stage[which]);
   c->d_stage[which] = nullptr;
+  c->d_cap[which] = 0;
   size_t n = grow(c->d_cap[which], bytes);
-  RDK_HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&c->d_stage[which]), n));
+  int rc = dev_alloc(&c->d_stage[which], n);
+  if (rc) return rc;
   c->d_cap[which] = n;
   return 0;
 }
 
+int scratch_acquire(Ctx *c, int which, size_t bytes, hipStream_t s) {
+  if (!c->d_done[which])
+    RDK_HIP_CHECK(hipEventCreateWithFlags(&c->d_done[which], hipEventDisableTiming));
+  if (c->d_cap[which] < bytes) {
+    // the previous user may still be running on another stream: wait for it alone
+    if (c->d_used[which]) RDK_HIP_CHECK(hipEventSynchronize(c->d_done[which]));
+    if (c->d_stage[which]) (void)hipFree(c->d_stage[which]);
+    c->d_stage[which] = nullptr;
+    c->d_cap[which] = 0;
+    c->d_used[which] = false;
+    size_t n = grow(0, bytes);
+    int rc = dev_alloc(&c->d_stage[which], n);
+    if (rc) return rc;
+    c->d_cap[which] = n;
+  } else if (c->d_used[which] && c->d_last[which] != s) {
+    RDK_HIP_CHECK(hipStreamWaitEvent(s, c->d_done[which], 0));
+  }
+  return 0;
+}
+
+int scratch_release(Ctx *c, int which, hipStream_t s) {
+  RDK_HIP_CHECK(hipEventRecord(c->d_done[which], s));
+  c->d_last[which] = s;
+  c->d_used[which] = true;
+  return 0;
+}
+
+// drop-in symbols only (c->stream, idle between calls)
 int ensure_desc(Ctx *c, size_t bytes) {
   if (c->d_desc_cap >= bytes) return 0;
   if (c->d_desc) {
-    (void)hipDeviceSynchronize();
     (void)hipFree(c->d_desc);
     (void)hipHostFree(c->h_desc);
   }
-  size_t n = grow(c->d_desc_cap, bytes);
-  RDK_HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&c->d_desc), n));
+  c->d_desc = nullptr;
+  c->h_desc = nullptr;
+  c->d_desc_cap = 0;
+  size_t n = grow(0, bytes);
+  int rc = dev_alloc(&c->d_desc, n);
+  if (rc) return rc;
   RDK_HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&c->h_desc), n, hipHostMallocDefault));
   c->d_desc_cap = n;
   return 0;
@@ -185,5 +236,5 @@ RDK_API int rdk_hip_init(int device) {
 RDK_API const char *rdk_hip_last_error(void) { return rdk::last_error(); }
 
 RDK_API const char *rdk_hip_version(void) {
-  return "librdkafka_hip 0.1 gfx950 crc32c:wave-rotnib-lds lz4c:wave-exact lz4d:wave-serial";
+  return "librdkafka_hip 0.2 gfx950 crc32c:group16-bytetab-lds lz4c:wave-exact+round64-fast lz4hc:3-9 lz4d:seg64-parallel";
 }

@@ -622,6 +622,11 @@ static unsigned grid_waves(uint64_t waves, uint32_t wpb) {
   return b ? unsigned(b) : 1u;
 }
 
+void launch_decode(uint8_t *scratch, const uint8_t *d_in, const uint64_t *d_in_offs,
+                   const uint32_t *d_in_lens, uint8_t *d_out, const uint64_t *d_out_offs,
+                   const uint32_t *d_out_caps, uint32_t *d_out_lens, int32_t *d_status,
+                   uint32_t n, hipStream_t s);
+
 int lz4f_decompress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
                            const uint32_t *d_in_lens, uint8_t *d_out,
                            const uint64_t *d_out_offs, const uint32_t *d_out_caps,
@@ -630,13 +635,35 @@ int lz4f_decompress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_off
   const size_t fs_bytes = (size_t(n) * sizeof(FrameState) + 255) & ~size_t(255);
   const size_t bd_bytes = size_t(n) * kMaxDesc * sizeof(BlockDesc);
   const size_t wk_bytes = 256 + size_t(n) * kMaxDesc * sizeof(uint32_t);
-  int rc = ensure_dev(c, 1, fs_bytes + bd_bytes + wk_bytes);
+  int rc = scratch_acquire(c, kScratchDecode, fs_bytes + bd_bytes + wk_bytes, s);
   if (rc) return rc;
-  FrameState *fs = reinterpret_cast<FrameState *>(c->d_stage[1]);
-  BlockDesc *bd = reinterpret_cast<BlockDesc *>(c->d_stage[1] + fs_bytes);
-  uint32_t *work_count = reinterpret_cast<uint32_t *>(c->d_stage[1] + fs_bytes + bd_bytes);
+  uint8_t *scratch = c->d_stage[kScratchDecode];
+  RDK_HIP_CHECK(hipMemsetAsync(scratch + fs_bytes + bd_bytes, 0, sizeof(uint32_t), s));
+  launch_decode(scratch, d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_caps, d_out_lens,
+                d_status, n, s);
+  RDK_HIP_CHECK(hipGetLastError());
+  return scratch_release(c, kScratchDecode, s);
+}
+
+// The four kernels of one batch decode on stream s.  `scratch` holds the FrameState
+// array, the BlockDesc table and the work list, laid out as decode_scratch_bytes(n)
+// says; its work counter (the word after the BlockDesc table) must be zero.
+size_t decode_scratch_bytes(uint32_t n) {
+  const size_t fs_bytes = (size_t(n) * sizeof(FrameState) + 255) & ~size_t(255);
+  const size_t bd_bytes = size_t(n) * kMaxDesc * sizeof(BlockDesc);
+  return fs_bytes + bd_bytes + 256 + size_t(n) * kMaxDesc * sizeof(uint32_t);
+}
+
+void launch_decode(uint8_t *scratch, const uint8_t *d_in, const uint64_t *d_in_offs,
+                   const uint32_t *d_in_lens, uint8_t *d_out, const uint64_t *d_out_offs,
+                   const uint32_t *d_out_caps, uint32_t *d_out_lens, int32_t *d_status,
+                   uint32_t n, hipStream_t s) {
+  const size_t fs_bytes = (size_t(n) * sizeof(FrameState) + 255) & ~size_t(255);
+  const size_t bd_bytes = size_t(n) * kMaxDesc * sizeof(BlockDesc);
+  FrameState *fs = reinterpret_cast<FrameState *>(scratch);
+  BlockDesc *bd = reinterpret_cast<BlockDesc *>(scratch + fs_bytes);
+  uint32_t *work_count = reinterpret_cast<uint32_t *>(scratch + fs_bytes + bd_bytes);
   uint32_t *work = work_count + 64;
-  RDK_HIP_CHECK(hipMemsetAsync(work_count, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(lz4f_walk_kernel, dim3((n + 63) / 64), dim3(64), 0, s, d_in, d_in_offs,
                      d_in_lens, n, fs, bd, work_count, work);
   // persistent grid: as many workgroups per CU as the LDS rings and the 32 wave slots allow
@@ -652,8 +679,6 @@ int lz4f_decompress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_off
                      d_in_lens, d_out, d_out_offs, d_out_caps, n, fs);
   hipLaunchKernelGGL(lz4f_finish_kernel, dim3(grid_waves(n, 4)), dim3(256), 0, s, d_out,
                      d_out_offs, n, fs, bd, d_out_lens, d_status);
-  RDK_HIP_CHECK(hipGetLastError());
-  return 0;
 }
 
 }  // namespace rdk

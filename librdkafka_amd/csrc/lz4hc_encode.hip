@@ -567,40 +567,30 @@ void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const 
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, hipStream_t s);
 
-namespace {
-struct HcScratch {
-  int device = -1;
-  unsigned waves = 0;  // scratch slices allocated (grows to the largest grid launched)
-  uint8_t *p = nullptr;
-};
-thread_local HcScratch tl_hc;  // per calling thread, stream-ordered reuse
-}  // namespace
-
+// The hash/chain tables (kHcScratch bytes per wave) and the work-queue counter live in
+// the calling thread's kScratchHc region: calls on different streams are ordered by
+// scratch_acquire / scratch_release, so two streams never share the tables.
 int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, int level, hipStream_t s) {
   if (!n) return 0;
-  if (n > (0xFFFFFFFFu / kHcItems) - kHcGrid) return RDK_HIP_RESP_ERR__BAD_COMPRESSION;
+  if (n > (0xFFFFFFFFu / kHcItems) - kHcGrid) return set_error(RDK_HIP_E_INVAL, "too many frames");
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
   const uint64_t items = uint64_t(n) * kHcItems;
   const unsigned grid = unsigned(items < kHcGrid ? items : kHcGrid);
-  int dev = 0;
-  RDK_HIP_CHECK(hipGetDevice(&dev));
-  if (tl_hc.device != dev || !tl_hc.p || tl_hc.waves < grid) {
-    // a single drop-in frame needs 64 slices, a large batch the full grid
-    if (tl_hc.p && tl_hc.device == dev) RDK_HIP_CHECK(hipFree(tl_hc.p));
-    tl_hc.p = nullptr;
-    RDK_HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&tl_hc.p), kHcScratch * grid + 256));
-    tl_hc.device = dev;
-    tl_hc.waves = grid;
-  }
+  // a single drop-in frame needs 64 slices, a large batch the full grid
+  int rc = scratch_acquire(c, kScratchHc, size_t(kHcScratch) * grid + 256, s);
+  if (rc) return rc;
+  uint8_t *p = c->d_stage[kScratchHc];
   const int attempts = 1 << (level - 1);  // clTable rows 3..9: 4 .. 256
-  uint32_t *next_item = reinterpret_cast<uint32_t *>(tl_hc.p + kHcScratch * tl_hc.waves);
+  uint32_t *next_item = reinterpret_cast<uint32_t *>(p + size_t(kHcScratch) * grid);
   RDK_HIP_CHECK(hipMemsetAsync(next_item, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(lz4hc_compress_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
-                     d_in_lens, d_out, d_out_offs, n, attempts, tl_hc.p, next_item);
+                     d_in_lens, d_out, d_out_offs, n, attempts, p, next_item);
   lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s);
   RDK_HIP_CHECK(hipGetLastError());
-  return 0;
+  return scratch_release(c, kScratchHc, s);
 }
 
 }  // namespace rdk

@@ -5,9 +5,10 @@
 // device, runs the gfx950 kernels on the thread's own stream and copies the
 // result back into malloc() memory owned by the caller -- the ownership
 // contract of rdkafka_lz4.c (rd_free == free, rd.h:104-119).
-#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -43,6 +44,42 @@ static Ctx *ctx_or_die(const char *who) {
   return c;
 }
 
+// Stage `len` bytes already gathered in c->h_stage and CRC them.  The CRC symbols
+// return the checksum itself, so they have no way to report a device error: a failed
+// attempt is retried once after draining the device (a transient allocation or launch
+// failure), and only a second failure aborts, loudly.
+static uint32_t crc_or_die(Ctx *c, size_t len, uint32_t init, int kind, const char *who) {
+  uint32_t out = 0;
+  if (crc_staged(c, len, init, &out, kind) == 0) return out;
+  fprintf(stderr, "librdkafka_hip: %s: %s; retrying\n", who, last_error());
+  (void)hipDeviceSynchronize();
+  (void)hipGetLastError();
+  if (crc_staged(c, len, init, &out, kind)) fatal(who);
+  return out;
+}
+
+// The LZ4 symbols do have an error channel (rdkafka_lz4.c returns
+// rd_kafka_resp_err_t): a device failure becomes __CRIT_SYS_RESOURCE (no device, out
+// of memory) or __BAD_COMPRESSION (anything else), never an abort.  The writer then
+// sends the MessageSet uncompressed (rdkafka_msgset_writer.c:1175-1176) and the reader
+// raises a consumer error for the batch (rdkafka_msgset_reader.c:517-526).  The first
+// failure of each kind is reported on stderr.
+static std::atomic<int> g_reported{0};
+static rd_kafka_resp_err_t lz4_err(int rc, const char *who) {
+  if (rc <= -100) return rc;  // already an rd_kafka_resp_err_t
+  const int bit = (rc == RDK_HIP_E_NODEV) ? 1 : (rc == RDK_HIP_E_NOMEM) ? 2 : 4;
+  if (!(g_reported.fetch_or(bit) & bit))
+    fprintf(stderr, "librdkafka_hip: %s failed on the device: %s\n", who, last_error());
+  return (rc == RDK_HIP_E_NODEV || rc == RDK_HIP_E_NOMEM) ? RDK_HIP_RESP_ERR__CRIT_SYS_RESOURCE
+                                                            : RDK_HIP_RESP_ERR__BAD_COMPRESSION;
+}
+
+static void slice_drain(rd_slice_t *slice) {  // leave the slice consumed, as the reference does
+  const void *skip;
+  while (slice_reader(slice, &skip)) {
+  }
+}
+
 }  // namespace rdk
 
 using namespace rdk;
@@ -54,9 +91,7 @@ RDK_API uint32_t crc32c(uint32_t crc, const void *buf, size_t len) {
   if (len == 0) return crc;  // pre/post inversions cancel (crc32c.c:102,133)
   if (ensure_host(c, len)) fatal("crc32c: pinned staging");
   std::memcpy(c->h_stage, buf, len);
-  uint32_t out = 0;
-  if (crc_staged(c, len, crc, &out, kCrcKind32C)) fatal("crc32c");
-  return out;
+  return crc_or_die(c, len, crc, kCrcKind32C, "crc32c");
 }
 
 // iovec gather (the rdbuf.c:1099-1101 / :1118-1119 loops) into the pinned staging buffer;
@@ -71,9 +106,7 @@ static uint32_t slice_crc(rd_slice_t *slice, int kind, const char *who) {
     std::memcpy(c->h_stage + of, p, rlen);
     of += rlen;
   }
-  uint32_t out = 0;
-  if (crc_staged(c, of, 0u, &out, kind)) fatal(who);
-  return out;
+  return crc_or_die(c, of, 0u, kind, who);
 }
 
 RDK_API uint32_t rd_slice_crc32c(rd_slice_t *slice) {
@@ -88,37 +121,36 @@ RDK_API uint32_t rd_slice_crc32(rd_slice_t *slice) {
 }
 
 // ------------------------------------------------------------------- LZ4F
-typedef rd_kafka_resp_err_t (*lz4c_fn)(rd_kafka_broker_t *, int, int, rd_slice_t *, void **,
-                                       size_t *);
-
 RDK_API rd_kafka_resp_err_t rd_kafka_lz4_compress(rd_kafka_broker_t *rkb, int proper_hc,
                                                   int comp_level, rd_slice_t *slice,
                                                   void **outbuf, size_t *outlenp) {
+  (void)rkb;
   *outbuf = nullptr;
   if (comp_level >= 10) {
-    // LZ4HC optimal (lz4hc.c:1278, levels 10..12) is not implemented by the
-    // engine: hand the call to the next definition (librdkafka's own) if any.
-    lz4c_fn next = reinterpret_cast<lz4c_fn>(dlsym(RTLD_NEXT, "rd_kafka_lz4_compress"));
-    if (next && next != &rd_kafka_lz4_compress)
-      return next(rkb, proper_hc, comp_level, slice, outbuf, outlenp);
-    const void *skip;
-    while (slice_reader(slice, &skip)) {  // consume like the reference would
-    }
+    // LZ4HC optimal (lz4hc.c:1278, levels 10..12) is not implemented by the engine
+    slice_drain(slice);
+    set_error(RDK_HIP_E_INVAL, "compression.level %d (LZ4HC optimal) is not implemented", comp_level);
     return RDK_HIP_RESP_ERR__BAD_COMPRESSION;
   }
-  Ctx *c = ctx_or_die("rd_kafka_lz4_compress");
+  Ctx *c = ctx();
+  if (!c) {
+    slice_drain(slice);
+    return lz4_err(RDK_HIP_E_NODEV, "rd_kafka_lz4_compress");
+  }
   const size_t total = slice_remains(slice);
-  if (ensure_host(c, total ? total : 1)) fatal("rd_kafka_lz4_compress: pinned staging");
+  int rc = ensure_host(c, total ? total : 1);
+  if (rc) {
+    slice_drain(slice);
+    return lz4_err(rc, "rd_kafka_lz4_compress");
+  }
   size_t of = 0, rlen;
   const void *p;
   while ((rlen = slice_reader(slice, &p))) {  // rdkafka_lz4.c:390 loop, gathered
     std::memcpy(c->h_stage + of, p, rlen);
     of += rlen;
   }
-  int rc = lz4f_compress_host(c, of, proper_hc, comp_level, outbuf, outlenp);
-  if (rc < -100) return rc;  // rd_kafka_resp_err_t
-  if (rc) fatal("rd_kafka_lz4_compress");
-  return RDK_HIP_RESP_ERR_NO_ERROR;
+  rc = lz4f_compress_host(c, of, proper_hc, comp_level, outbuf, outlenp);
+  return rc ? lz4_err(rc, "rd_kafka_lz4_compress") : RDK_HIP_RESP_ERR_NO_ERROR;
 }
 
 RDK_API rd_kafka_resp_err_t rd_kafka_lz4_decompress(rd_kafka_broker_t *rkb, int proper_hc,
@@ -127,10 +159,9 @@ RDK_API rd_kafka_resp_err_t rd_kafka_lz4_decompress(rd_kafka_broker_t *rkb, int 
   (void)rkb;
   (void)Offset;
   *outbuf = nullptr;
-  Ctx *c = ctx_or_die("rd_kafka_lz4_decompress");
+  Ctx *c = ctx();
+  if (!c) return lz4_err(RDK_HIP_E_NODEV, "rd_kafka_lz4_decompress");
   int rc = lz4f_decompress_host(c, proper_hc, reinterpret_cast<uint8_t *>(inbuf), inlen, outbuf,
                                 outlenp);
-  if (rc < -100) return rc;
-  if (rc) fatal("rd_kafka_lz4_decompress");
-  return RDK_HIP_RESP_ERR_NO_ERROR;
+  return rc ? lz4_err(rc, "rd_kafka_lz4_decompress") : RDK_HIP_RESP_ERR_NO_ERROR;
 }

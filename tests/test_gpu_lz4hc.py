@@ -95,3 +95,26 @@ def test_hc_optimal_levels_rejected(engine):
     n = torch.full((1,), 100, dtype=torch.int32, device="cuda")
     with pytest.raises(engine.EngineError):
         engine.lz4f_compress_batch(d, o, n, d, o, n, level=10)
+
+
+def test_batch_hc_many_frames_queue_and_scratch_growth(engine, oracle_mod):
+    """96 x 1 MiB at level 9 after a one-frame call: 1536 block items over a grid that was
+    last sized for 16 (the scratch grows), and at the full 4096-wave grid every wave takes
+    its blocks from the work queue.  Four distinct inputs rotate, so the oracle runs 4x."""
+    import torch
+    distinct = [W.gen_json(1 << 20, 90 + i) for i in range(4)]
+    want = [oracle_mod.rdk_lz4_compress(b, comp_level=9)[1] for b in distinct]
+    for inputs in ([distinct[0]], [distinct[i % 4] for i in range(96)]):
+        hbuf, hoffs = _pack(inputs)
+        d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
+        in_offs = torch.tensor(hoffs, dtype=torch.int64, device="cuda")
+        in_lens = torch.tensor([len(b) for b in inputs], dtype=torch.int32, device="cuda")
+        bound = (engine.lz4f_compress_bound(1 << 20) + 63) // 64 * 64
+        d_out = torch.zeros(len(inputs) * bound + 256, dtype=torch.uint8, device="cuda")
+        out_offs = torch.arange(len(inputs), dtype=torch.int64, device="cuda") * bound
+        out_lens = torch.zeros(len(inputs), dtype=torch.int32, device="cuda")
+        engine.lz4f_compress_batch(d_in, in_offs, in_lens, d_out, out_offs, out_lens, level=9)
+        host = bytes(d_out.cpu().numpy())
+        fl = out_lens.cpu().numpy()
+        for i in range(len(inputs)):
+            assert host[i * bound:i * bound + fl[i]] == want[i % 4], (len(inputs), i)

@@ -73,10 +73,14 @@ def test_producer_order_and_busy(engine):
     hdr = W.v2_header(0, 61 + len(rec))
     assert p.produce(hdr, rec, 0) == 0
     assert p.produce(hdr, rec, 1) == 0          # launches slot 0, fills slot 1
-    assert p.produce(hdr, rec, 2) == engine.E_BUSY or True
+    # slot 1 is launched to make room, slot 0 has not been polled: the ring is full and
+    # the batch is refused (a slot stays in flight until poll() has handed it back)
+    assert p.produce(hdr, rec, 2) == engine.E_BUSY
     order = []
-    p.flush()
     while len(order) < 2:
         order += [c for c, _, _ in p.poll(block=True)]
     assert order == [0, 1]
+    assert p.produce(hdr, rec, 2) == 0          # room again
+    p.flush()
+    assert [c for c, _, _ in p.poll(block=True)] == [2]
     p.close()

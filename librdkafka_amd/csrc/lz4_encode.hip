@@ -8,7 +8,23 @@
 // One wavefront (one 64-thread workgroup) per independent 64 KiB block with
 // its own 8192-entry u16 hash table in LDS (16 KiB -> 10 blocks per CU).  The
 // greedy parse is emulated EXACTLY, so frames are byte-identical to the
-// reference's:
+// reference's.  Two engines:
+//
+//  * window_block() (acceleration 1, i.e. compression.level 0..2): the parse runs
+//    in WINDOWS of 64 consecutive positions, one per lane.  Every lane loads its
+//    own 36 source bytes and its table candidate's 36 bytes once, verifies
+//    MINMATCH, measures the match (up to 28 bytes) and the catch-up (up to 4)
+//    from registers; a scalar walk then replays the sequential loop over those
+//    per-lane results: which positions are probed and inserted, the first
+//    verifying probe, catch-up, ip-2 insertion and the immediate re-test after a
+//    match (lz4.c:1084-1134).  A candidate inserted earlier in the same window
+//    is found with a hash-equality mask over the lanes.  Several sequences per
+//    window cost two gathers, not a chain of dependent loads each; their bytes
+//    are emitted together at wave-prefix-sum positions.  Searches that outlast
+//    the stride-1 probes (lz4.c:896-905) continue in generic_search().
+//
+//  * compress_block() (acceleration > 1, negative compression.level): one
+//    sequence at a time, every step through memory:
 //   * the match search evaluates 64 consecutive probe positions at once
 //     (the skip schedule step = searchMatchNb++ >> 6 is reproduced by a lane
 //     prefix-sum); each lane's candidate is the latest earlier probe with the
@@ -24,8 +40,11 @@
 // and slides the blocks down into stream order.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "lz4_device.h"
+#include "lz4_wave.h"
 
 namespace rdk {
 
@@ -34,6 +53,9 @@ constexpr uint32_t kSlot = kLz4Block + 4;  // worst-case bytes per block in a fr
 constexpr uint32_t kHashLog = 13;          // LZ4_HASHLOG+1 for byU16 (lz4.c:633)
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t lz4_hash(uint32_t seq) {  // LZ4_hash4, lz4.c:631
   return (seq * 2654435761u) >> (32 - kHashLog);
@@ -242,14 +264,488 @@ last_literals : {  // lz4.c:1141-1166
   return op;
 }
 
+// ===================================================================== windows
+// The search loop of lz4.c:909-957 from probe index `cbase` at position `fwd`, 64 probes
+// per step (strides above 1 included).  true: a probe verified, P / cand are set and the
+// table holds every probe up to P; false: forwardIp passed mflimitPlusOne (last literals).
+__device__ __forceinline__ bool generic_search(uintptr_t src, int mflimitPlusOne, uint32_t A64,
+                                               int fwd, uint32_t cbase, lds_u16 *table,
+                                               int lane, int &P_out, int &cand_out) {
+  for (;;) {
+    const uint32_t c = cbase + uint32_t(lane);
+    const uint32_t s = (c == 0) ? 1u : ((A64 + c - 1u) >> 6);
+    const uint32_t incl = wave_incl_scan(s, lane);
+    const int P = fwd + int(incl - s);
+    const int Pn = fwd + int(incl);
+    const bool valid = Pn <= mflimitPlusOne;
+    const uint64_t vmask = ballot(valid);
+    const uint32_t seq = valid ? ld32u(src + uint32_t(P)) : 0u;
+    const uint32_t h = lz4_hash(seq);
+    uint64_t eq = vmask;
+#pragma unroll
+    for (uint32_t bit = 0; bit < kHashLog; ++bit) {
+      const bool hb = (h >> bit) & 1u;
+      const uint64_t bm = ballot(hb);
+      eq &= hb ? bm : ~bm;
+    }
+    const uint64_t lower = eq & ((1ull << lane) - 1ull);
+    const int pred = lower ? 63 - __builtin_clzll(lower) : 0;
+    const int predP = __shfl(P, pred);
+    const int cand = lower ? predP : int(table[h]);
+    const bool m = valid && ld32u(src + uint32_t(cand)) == seq;
+    const uint64_t mm = ballot(m);
+    const int f = ffs64(mm);
+    const int e = ffs64(~vmask);
+    if (f < e) {
+      const uint64_t upto = (2ull << f) - 1ull;
+      const uint64_t later = eq & ~((2ull << lane) - 1ull) & upto;
+      if (lane <= f && !later) table[h] = uint16_t(P);
+      P_out = __builtin_amdgcn_readlane(P, f);
+      cand_out = __builtin_amdgcn_readlane(cand, f);
+      return true;
+    }
+    if (e < 64) return false;
+    {
+      const uint64_t later = eq & ~((2ull << lane) - 1ull);
+      if (!later) table[h] = uint16_t(P);
+    }
+    fwd = __builtin_amdgcn_readlane(Pn, 63);
+    cbase += 64u;
+  }
+}
+
+constexpr int kRegLen = 28;   // match bytes a lane measures from its two register windows
+constexpr int kRegBack = 4;   // catch-up bytes a lane measures from them
+constexpr uint32_t kShortLit = 16;  // literal runs copied by their own lane
+
+enum WinMode { W_SEARCH = 0, W_POSTMATCH = 1, W_FORCED = 2 };
+enum WinStatus { W_CONTINUE = 0, W_LAST = 1, W_OVERFLOW = 2 };
+
+struct WinBlock {
+  uintptr_t src, dst;
+  rsrc_t r;   // the block's dwords (reads outside return 0)
+  rsrc_t w;   // the block's output slot (byte stores; parked lanes write nothing)
+  uint32_t sa;  // src & 3: byte offset of position 0 inside the read resource
+  int n, mfl1, mlim, olimit;  // size, mflimitPlusOne, matchlimit, dstCapacity
+  int ip;      // next probe (W_SEARCH) / end of the last match (W_POSTMATCH)
+  int cnt;     // probes already made in the current search
+  int anchor, op;
+  int mode;    // how the next window starts
+  // source ring in LDS: virtual positions (position + sa) [H - kRingBytes, H) are at
+  // ring[v & (kRingBytes-1)].  `pend` is the chunk at H, loaded one fill ahead.
+  lds_u32 *ring;
+  int H;
+  u32x4 pend;
+};
+
+constexpr uint32_t kRingBytes = 4096, kRingChunk = 1024;
+
+// ring[H, H+1 KiB) <- pend; the load of the following chunk is issued at once
+__device__ __forceinline__ void ring_fill(WinBlock &b, int lane) {
+  typedef __attribute__((address_space(3))) u32x4 lds_u4v;
+  const uint32_t at = (uint32_t(b.H) & (kRingBytes - 1u)) + 16u * uint32_t(lane);
+  *(lds_u4v *)((lds_u8 *)b.ring + at) = b.pend;
+  b.H += int(kRingChunk);
+  b.pend = __builtin_amdgcn_raw_buffer_load_b128(b.r, uint32_t(b.H) + 16u * uint32_t(lane), 0, 0);
+  asm volatile("" ::: "memory");
+}
+
+// nine dwords around virtual position v (4-aligned a = v & ~3): a-4 .. a+28, from the ring.
+// Eight consecutive dwords from the ring index of a; the few lanes whose window runs over
+// the end of the ring read again with every index wrapped (the straight reads past the
+// end land in the hash table behind the ring: harmless).
+__device__ __forceinline__ void ring_load9(const WinBlock &b, uint32_t a, uint32_t d[9]) {
+  const uint32_t at = a & (kRingBytes - 1u);
+  d[0] = *(lds_u32 *)((lds_u8 *)b.ring + ((a - 4u) & (kRingBytes - 1u)));
+  lds_u32 *p = (lds_u32 *)((lds_u8 *)b.ring + at);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d[k + 1] = p[k];
+  const bool wraps = at > kRingBytes - 32u;
+  if (ballot(wraps)) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const uint32_t v = *(lds_u32 *)((lds_u8 *)b.ring + ((at + 4u * uint32_t(k)) & (kRingBytes - 1u)));
+      if (wraps) d[k + 1] = v;
+    }
+  }
+}
+
+__device__ __forceinline__ bool ring_has(const WinBlock &b, int v_lo, int v_hi) {  // [v_lo, v_hi)
+  return v_lo >= b.H - int(kRingBytes) && v_hi <= b.H;
+}
+
+// equal bytes a[i]==b[i], i < limit, 64 per wave step; a / c are block positions.  Steps
+// whose bytes are all in the ring read LDS, the others global memory.
+__device__ __forceinline__ int win_count_fwd(const WinBlock &b, int a, int c, int limit, int lane) {
+  int cnt = 0;
+  while (cnt < limit) {
+    const int l = cnt + lane;
+    const int va = a + cnt + int(b.sa), vc = c + cnt + int(b.sa);
+    uint32_t x, y;
+    if (ring_has(b, vc, vc + 64) && ring_has(b, va, va + 64)) {
+      x = ((lds_u8 *)b.ring)[uint32_t(va + lane) & (kRingBytes - 1u)];
+      y = ((lds_u8 *)b.ring)[uint32_t(vc + lane) & (kRingBytes - 1u)];
+    } else {
+      x = l < limit ? ldb(b.src + uint32_t(a + l)) : 0u;
+      y = l < limit ? ldb(b.src + uint32_t(c + l)) : 1u;
+    }
+    const uint64_t m = ballot(l < limit && x == y);
+    const int run = m == ~0ull ? 64 : __builtin_ctzll(~m);
+    cnt += run;
+    if (run < 64) break;
+  }
+  return cnt;
+}
+
+__device__ __forceinline__ uint64_t bits_below(int x) {  // lanes [0, x), x in 0..64
+  return x >= 64 ? ~0ull : ((1ull << x) - 1ull);
+}
+__device__ __forceinline__ uint64_t bits_range(int a, int b) {  // lanes [a, b)
+  return a >= b ? 0ull : (bits_below(b) & ~bits_below(a));
+}
+
+// One window of 64 positions from w0.  See the file comment; tests/sim/lz4_window_sim.cpp
+// is the same walk with the lanes as arrays.
+__device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand, lds_u16 *table,
+                                           int lane) {
+  const int mode = b.mode;
+  // ---------------------------------------------------------------- per lane
+  const int i = w0 + lane;
+  const bool act = i <= b.n - kLz4MFLimit;  // position + 1 <= mflimitPlusOne
+  // the ring covers this window's own bytes: positions w0 .. w0+63 and 35 bytes beyond
+  while (b.H < w0 + int(b.sa) + 64 + 36) ring_fill(b, lane);
+  uint32_t xd[9], yt[9];
+  ring_load9(b, (uint32_t(i) + b.sa) & ~3u, xd);
+  const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
+  const uint32_t seq = __builtin_amdgcn_alignbyte(xd[2], xd[1], shi);
+  const uint32_t h = lz4_hash(seq);
+  int tc = act ? int(table[h]) : 0;
+  if (mode == W_FORCED && lane == 0) tc = forced_cand;
+  // the candidate's 36 bytes: from the ring when it is that recent, else from memory
+  const uint32_t ac = (uint32_t(tc) + b.sa) & ~3u;
+  const bool far = act && int(ac) - 4 < b.H - int(kRingBytes);
+  ring_load9(b, ac, yt);
+  if (ballot(far)) {
+    uint32_t g[9];
+    load9(b.r, far ? ac : kNoLoad, g);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) yt[k] = far ? g[k] : yt[k];
+  }
+  // lanes with the same hash (the candidate may be a position inserted in this window)
+  const uint64_t ACT = ballot(act);
+  uint64_t eq = ACT;
+#pragma unroll
+  for (uint32_t bit = 0; bit < kHashLog; ++bit) {
+    const bool hb = (h >> bit) & 1u;
+    const uint64_t bm = ballot(hb);
+    eq &= hb ? bm : ~bm;
+  }
+  if (!act) eq = 0;
+  const uint64_t DUP = ballot((eq & ((1ull << lane) - 1ull)) != 0);
+  const uint32_t shc = (uint32_t(tc) + b.sa) & 3u;
+  const bool tver = act && seq == __builtin_amdgcn_alignbyte(yt[2], yt[1], shc);
+  const uint64_t VT = ballot(tver);
+  int len = kRegLen;
+#pragma unroll
+  for (int k = 6; k >= 1; --k) {
+    const uint32_t z = __builtin_amdgcn_alignbyte(xd[k + 2], xd[k + 1], shi) ^
+                       __builtin_amdgcn_alignbyte(yt[k + 2], yt[k + 1], shc);
+    if (z) len = 4 * k + (__builtin_ctz(z) >> 3);
+  }
+  if (len > b.mlim - i) len = b.mlim - i;  // LZ4_count stops at matchlimit
+  const uint32_t back = __builtin_amdgcn_alignbyte(xd[1], xd[0], shi);  // bytes i-4 .. i-1
+  const uint32_t xb = back ^ __builtin_amdgcn_alignbyte(yt[1], yt[0], shc);
+  int bkr = xb ? int(__builtin_clz(xb) >> 3) : kRegBack;
+  if (bkr > tc) bkr = tc;  // nothing in front of the block
+  const int NA = ~ACT ? __builtin_ctzll(~ACT) : 64;  // first lane that may not be probed
+
+  // one readlane per sequence fetches the lane's candidate, match length and catch-up
+  const uint32_t pk = uint32_t(tc) | (uint32_t(len) << 16) | (uint32_t(bkr) << 24);
+  const uint64_t VD = VT | DUP;  // lanes >= NA have neither bit
+
+  // ------------------------------------------------------------- scalar walk
+  // One loop iteration per sequence: the pending match (lz4.c:958-1081), then ip-2
+  // insertion and the re-test of ip (lz4.c:1084-1134), then the search for the next match
+  // (lz4.c:909-957).  The scalar unit is shared by the CU's waves, so the common path is
+  // kept to a few dozen scalar instructions; lanes whose hash repeats inside the window
+  // (DUP) take the slow lookup.
+  const int anchor_in = b.anchor;
+  uint64_t INS = 0, chosen = 0;
+  int L_cand = 0, L_len = 0, L_bk = 0;  // per lane: the sequence whose match starts here
+  int anchor = b.anchor, cnt = b.cnt;
+  int q = 0, x = 0, cand = 0, ipn = 0;
+  bool inwin = false, ver = false;
+  int st = W_CONTINUE;
+  b.mode = W_SEARCH;
+
+  // candidate of lane lx given the inserts so far: the latest inserted lane of this window
+  // with the same hash, else the table entry read when the window started
+#define RDK_WIN_LOOKUP(lx)                                                                  \
+  do {                                                                                      \
+    const uint64_t eqx = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(eq >> 32), (lx)))) << 32) | \
+                         uint32_t(__builtin_amdgcn_readlane(int(eq), (lx)));                \
+    const uint64_t m_ = eqx & INS & bits_below(lx);                                         \
+    if (m_) {                                                                               \
+      const int j_ = 63 - __builtin_clzll(m_);                                              \
+      cand = w0 + j_;                                                                       \
+      inwin = true;                                                                         \
+      ver = __builtin_amdgcn_readlane(int(seq), j_) == __builtin_amdgcn_readlane(int(seq), (lx)); \
+    } else {                                                                                \
+      inwin = false;                                                                        \
+      ver = (VT >> (lx)) & 1ull;                                                            \
+    }                                                                                       \
+  } while (0)
+
+  bool have = false;  // a verified match at lane x is pending
+  bool post = false;  // a match just ended at ipn
+  if (mode == W_POSTMATCH) {
+    ipn = w0 + 2;
+    post = true;
+  } else if (mode == W_FORCED) {
+    x = 0;  // lane 0's candidate was set to forced_cand above
+    have = true;
+  }
+  for (;;) {
+    if (have) {
+      have = false;
+      const int P = w0 + x;
+      const uint32_t pkx = uint32_t(__builtin_amdgcn_readlane(int(pk), x));
+      if (!inwin) cand = int(pkx & 0xFFFFu);
+      const int blim = P - anchor < cand ? P - anchor : cand;  // lz4.c:958: ip>anchor, match>lowLimit
+      int fl, bk;
+      if (inwin) {
+        fl = win_count_fwd(b, P + 4, cand + 4, b.mlim - (P + 4), lane);
+        bk = wave_count_back(b.src + uint32_t(P), b.src + uint32_t(cand), blim, lane);
+      } else {
+        const int lx = int((pkx >> 16) & 0xFFu), bx = int(pkx >> 24);
+        fl = lx - 4;
+        if (lx == kRegLen && P + kRegLen < b.mlim)
+          fl += win_count_fwd(b, P + kRegLen, cand + kRegLen, b.mlim - P - kRegLen, lane);
+        bk = bx < blim ? bx : blim;
+        if (bx == kRegBack && blim > kRegBack)
+          bk = kRegBack + wave_count_back(b.src + uint32_t(P - kRegBack),
+                                          b.src + uint32_t(cand - kRegBack), blim - kRegBack, lane);
+      }
+      if (lane == x) {
+        L_cand = cand;
+        L_len = 4 + fl;
+        L_bk = bk;
+      }
+      chosen |= 1ull << x;
+      ipn = P + 4 + fl;
+      anchor = ipn;
+      if (ipn >= b.mfl1) {  // lz4.c:1081
+        st = W_LAST;
+        break;
+      }
+      post = true;
+    }
+    if (post) {
+      post = false;
+      const int r = ipn - 2 - w0;
+      if (r >= 62) {  // the re-test position lies beyond this window
+        b.ip = ipn;
+        b.mode = W_POSTMATCH;
+        break;
+      }
+      x = r + 2;
+      INS |= 5ull << r;  // LZ4_putPosition(ip-2), lz4.c:1084, and the re-tested ip itself
+      if ((DUP >> x) & 1ull) {
+        RDK_WIN_LOOKUP(x);
+      } else {
+        inwin = false;
+        ver = (VT >> x) & 1ull;
+      }
+      if (ver) {  // immediate match: no literals, no catch-up (anchor == position)
+        have = true;
+        continue;
+      }
+      q = x + 1;
+      cnt = 0;
+    }
+    // search from lane q, whose probe index is cnt; lanes from xlim on have strides above 1
+    const int xlim = q + 65 - cnt;
+    uint64_t cm = q < 64 ? VD & (~0ull << q) : 0ull;
+    if (xlim < 64) cm &= bits_below(xlim);
+    if (!cm) {  // no candidate left in this window
+      int stop = NA;  // <= 64
+      int why = NA < 64 ? 1 : 0;  // 1: last literals, 0: window end
+      if (xlim <= stop) {         // 2: strides above 1 from here on
+        stop = xlim;
+        why = 2;
+      }
+      INS |= bits_range(q, stop);
+      if (why == 1) {
+        st = W_LAST;
+      } else {
+        b.ip = w0 + stop;
+        b.cnt = cnt + (stop - q);
+      }
+      break;
+    }
+    x = __builtin_ctzll(cm);
+    INS |= (~0ull << q) & ~(~1ull << x);  // lanes q..x are probed and inserted
+    cnt += x + 1 - q;
+    q = x + 1;
+    if ((DUP >> x) & 1ull) {
+      RDK_WIN_LOOKUP(x);
+      have = ver;
+    } else {  // x has no earlier lane with its hash: its table candidate verified (VT)
+      inwin = false;
+      have = true;
+    }
+  }
+#undef RDK_WIN_LOOKUP
+
+  // ------------------------------------------------------------ table update
+  // every inserted lane; the latest position per hash wins
+  if (st != W_LAST) {
+    const bool ins = (INS >> lane) & 1ull;
+    const uint64_t later = eq & INS & ~bits_below(lane + 1);
+    if (ins && !later) table[h] = uint16_t(i);
+    asm volatile("" ::: "memory");
+  }
+  // ---------------------------------------------------------------- emission
+  // Each chosen lane writes its own token, literal-length bytes, literals, offset and
+  // match-length bytes at a wave-prefix-sum position.  Every window runs the same store
+  // instructions (parked lanes write nothing).
+  {
+    const bool ch = (chosen >> lane) & 1ull;
+    const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
+    const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
+    const int pend = __shfl(i + L_len, pl);  // end of the previous chosen match
+    const int prev = lowc ? pend : anchor_in;  // this sequence's anchor
+    const uint32_t lit = ch ? uint32_t(i - L_bk - prev) : 0u;
+    const uint32_t mc = uint32_t(L_len + L_bk - 4);
+    const uint32_t lext = ext_bytes(lit);
+    const uint32_t sz = ch ? 3u + lit + lext + ext_bytes(mc) : 0u;
+    uint32_t tot;
+    const uint32_t o = wave_excl_scan(sz, tot);
+    const uint32_t tp = uint32_t(b.op) + o;  // token position in the block output
+    const uint32_t lp = tp + 1u + lext;      // first literal
+    const uint32_t fp = lp + lit;            // offset field
+    // limitedOutput, lz4.c:964 (literals) and lz4.c:1044 (match length)
+    const bool ov = ch && (int(tp + 1u + lit + (2u + 1u + kLz4LastLiterals) + lit / 255u) > b.olimit ||
+                           int(fp + 2u + (1u + kLz4LastLiterals) + (mc + 240u) / 255u) > b.olimit);
+    if (ballot(ov)) return W_OVERFLOW;
+    __builtin_amdgcn_raw_buffer_store_b8(
+        uint8_t(((lit < 15u ? lit : 15u) << 4) | (mc < 15u ? mc : 15u)), b.w, ch ? tp : kNoLoad, 0, 0);
+    // up to 4 literals (with the catch-up) sit in the lane's own back dword
+    const bool in_reg = ch && lit + uint32_t(L_bk) <= 4u;
+    const uint32_t first = 4u - uint32_t(L_bk) - lit;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(back >> (8u * ((first + k) & 3u))), b.w,
+                                           (in_reg && k < lit) ? lp + k : kNoLoad, 0, 0);
+    const uint32_t off = uint32_t(i - L_cand);
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), b.w, ch ? fp : kNoLoad, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), b.w, ch ? fp + 1u : kNoLoad, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(mc - 15u), b.w,
+                                         (ch && mc >= 15u && mc < 270u) ? fp + 2u : kNoLoad, 0, 0);
+    // rare shapes, each behind a wave-uniform test
+    if (ballot(ch && lit >= 15u)) {
+      if (ch && lit >= 15u) put_len(b.dst + tp + 1u, lit);
+    }
+    if (ballot(ch && mc >= 270u)) {
+      if (ch && mc >= 270u) put_len(b.dst + fp + 2u, mc);
+    }
+    const uint32_t lstart = uint32_t(prev);
+    const uint32_t la = (lstart + b.sa) & ~3u;
+    const bool need_win = ch && !in_reg && lit <= kShortLit && int(la) >= b.H - int(kRingBytes);
+    if (ballot(need_win)) {  // 5..16 literals: one 20-byte window per lane, from the ring
+      uint32_t wv[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        wv[k] = *(lds_u32 *)((lds_u8 *)b.ring + ((la + 4u * uint32_t(k)) & (kRingBytes - 1u)));
+      const uint32_t sh = (lstart + b.sa) & 3u;
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], sh);
+#pragma unroll
+      for (uint32_t k = 0; k < kShortLit; ++k)
+        __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), b.w,
+                                             (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
+    }
+    uint64_t longm = ballot(ch && !in_reg && !need_win);  // long runs: the whole wave copies them
+    while (longm) {
+      const int j = __builtin_ctzll(longm);
+      longm &= longm - 1;
+      const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
+      const uint32_t jp = __builtin_amdgcn_readlane(lp, j);
+      const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
+      wave_copy_bytes(b.dst + jp, b.src + js, jl, lane);
+    }
+    b.op += int(tot);
+  }
+  b.anchor = anchor;
+  return st;
+}
+
+// LZ4_compress_generic(byU16, limitedOutput, acceleration 1) in windows; table already
+// zeroed.  Returns the compressed size, or 0 when it does not fit in n-1 bytes.
+__device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, lds_u32 *ring,
+                            int lane) {
+  WinBlock b;
+  b.src = src;
+  b.dst = dst;
+  const uintptr_t lo = src & ~uintptr_t(3);
+  b.r = block_rsrc(lo, (src + uint32_t(n) + 3u) & ~uintptr_t(3));
+  b.w = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(dst), 0, n, 0x00020000);
+  b.sa = uint32_t(src & 3u);
+  b.n = n;
+  b.mfl1 = n - kLz4MFLimit + 1;
+  b.mlim = n - kLz4LastLiterals;
+  b.olimit = n - 1;  // LZ4F_makeBlock dstCapacity
+  b.ip = 1;          // position 0 goes into the zero entry it already holds (lz4.c:879)
+  b.cnt = 0;
+  b.anchor = 0;
+  b.op = 0;
+  b.mode = W_SEARCH;
+  b.ring = ring;
+  b.H = 0;
+  b.pend = __builtin_amdgcn_raw_buffer_load_b128(b.r, 16u * uint32_t(lane), 0, 0);
+  int forced = 0;
+  for (;;) {
+    int w0;
+    if (b.mode == W_SEARCH && b.cnt > 64) {  // strides above 1: the search continues probe by probe
+      int P, cand;
+      if (!generic_search(src, b.mfl1, 1u << 6, b.ip, uint32_t(b.cnt), table, lane, P, cand)) break;
+      asm volatile("" ::: "memory");
+      b.mode = W_FORCED;
+      forced = cand;
+      w0 = P;
+    } else {
+      w0 = b.mode == W_POSTMATCH ? b.ip - 2 : b.ip;
+    }
+    const int st = window_step(b, w0, forced, table, lane);
+    if (st == W_OVERFLOW) return 0;
+    if (st == W_LAST) break;
+  }
+  // last literals (lz4.c:1141-1166)
+  const uint32_t last = uint32_t(n - b.anchor);
+  if (b.op + int(last) + 1 + int((last + 255u - 15u) / 255u) > b.olimit) return 0;
+  if (lane == 0) {
+    uintptr_t p0 = dst + uint32_t(b.op);
+    stb(p0++, (last < 15u ? last : 15u) << 4);
+    if (last >= 15u) put_len(p0, last);
+  }
+  const int op = b.op + 1 + int(ext_bytes(last));
+  wave_copy_bytes(dst + uint32_t(op), src + uint32_t(b.anchor), last, lane);
+  return op + int(last);
+}
+
 // One wavefront per block.  Block k of frame f goes to the worst-case slot
 // at out_offs[f] + 7 + k*kSlot as [LE32 size word][payload]; a block stored
 // raw gets only its size word (payload is taken from the input later).
+template <bool WINDOWS>
 __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ out_offs, uint32_t n, int accel) {
-  __shared__ __attribute__((aligned(16))) uint16_t table_mem[1u << kHashLog];
+  // the source ring (windowed engine) sits in front of the hash table
+  constexpr uint32_t kRingLds = WINDOWS ? kRingBytes : 0u;
+  __shared__ __attribute__((aligned(16))) uint8_t lds_mem[kRingLds + (2u << kHashLog)];
+  uint16_t *table_mem = reinterpret_cast<uint16_t *>(lds_mem + kRingLds);
   lds_u16 *table = (lds_u16 *)table_mem;
   const int lane = threadIdx.x;
   const uint64_t items = uint64_t(n) * kEncMaxItems;
@@ -270,7 +766,8 @@ __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
         const u32x4e z = {0u, 0u, 0u, 0u};
         for (int i = lane; i < int((2u << kHashLog) / 16u); i += 64) t4[i] = z;
         asm volatile("" ::: "memory");
-        csize = compress_block(src, int(bn), slot + 4u, accel, table, lane);
+        csize = WINDOWS ? window_block(src, int(bn), slot + 4u, table, (lds_u32 *)lds_mem, lane)
+                        : compress_block(src, int(bn), slot + 4u, accel, table, lane);
       }
       if (lane == 0) {
         const uint32_t w = csize ? uint32_t(csize) : (bn | 0x80000000u);  // LZ4F_makeBlock
@@ -354,8 +851,15 @@ int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
   if (!n) return 0;
   uint64_t items = uint64_t(n) * kEncMaxItems;
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
-  hipLaunchKernelGGL(lz4_compress_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
-                     d_in_lens, d_out, d_out_offs, n, accel);
+  // RDK_HIP_LZ4_EXACT_SEQ=1 keeps the sequence-at-a-time engine for acceleration 1 too
+  // (A/B measurements of the same frames)
+  static const bool seq_only = getenv("RDK_HIP_LZ4_EXACT_SEQ") && atoi(getenv("RDK_HIP_LZ4_EXACT_SEQ"));
+  if (accel == 1 && !seq_only)
+    hipLaunchKernelGGL(lz4_compress_blocks_kernel<true>, dim3(grid), dim3(64), 0, s, d_in,
+                       d_in_offs, d_in_lens, d_out, d_out_offs, n, accel);
+  else
+    hipLaunchKernelGGL(lz4_compress_blocks_kernel<false>, dim3(grid), dim3(64), 0, s, d_in,
+                       d_in_offs, d_in_lens, d_out, d_out_offs, n, accel);
   lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;

@@ -1,0 +1,330 @@
+// lz4_window_sim.cpp -- host model of the windowed exact LZ4 block compressor
+// (librdkafka_amd/csrc/lz4_encode.hip, window_block()).
+//
+// TEST INFRASTRUCTURE.  The HIP kernel reproduces LZ4_compress_generic's greedy
+// parse (lz4.c:789-1177, byU16, acceleration 1) in windows of 64 consecutive
+// positions, one per lane, with a scalar walk over per-lane precomputed
+// candidates.  This file is the same algorithm with the 64 lanes as arrays and
+// the wave intrinsics as loops, so the parse logic (which positions are probed
+// and inserted, catch-up, the immediate re-test after a match, window hand-over,
+// the limitedOutput checks) can be checked against the oracle on a machine
+// without a GPU.  tests/test_window_sim.py compares its output byte for byte
+// with oracle/lz4_oracle.c on the same inputs.
+//
+// Build: g++ -O2 -shared -fPIC -o libwindowsim.so lz4_window_sim.cpp
+#include <cstdint>
+#include <cstring>
+
+namespace {
+
+constexpr int kMinMatch = 4, kLastLiterals = 5, kMFLimit = 12;
+constexpr int kRegLen = 28;   // match bytes a lane measures from its register windows
+constexpr int kRegBack = 4;   // catch-up bytes a lane measures from its register windows
+
+struct Block {
+  const uint8_t *src;
+  int n, mfl1, mlim, olimit;  // mflimitPlusOne, matchlimit, dstCapacity
+  uint8_t *dst;
+  uint16_t table[1 << 13];
+  int ip, cnt, anchor, op;
+  // statistics for the test: how often each path ran
+  long windows, generic, inwin, longfwd, longback;
+};
+
+inline uint32_t rd32(const uint8_t *p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+inline uint32_t hash13(uint32_t seq) { return (seq * 2654435761u) >> 19; }  // lz4.c:631, byU16
+
+inline int count_fwd(const Block &b, int a, int c, int limit) {  // equal bytes, at most limit
+  int k = 0;
+  while (k < limit && b.src[a + k] == b.src[c + k]) ++k;
+  return k;
+}
+inline int count_back(const Block &b, int a, int c, int limit) {  // equal bytes before a / c
+  int k = 0;
+  while (k < limit && b.src[a - 1 - k] == b.src[c - 1 - k]) ++k;
+  return k;
+}
+
+enum Mode { SEARCH = 0, POSTMATCH = 1, FORCED = 2 };
+enum Status { CONTINUE = 0, LAST = 1, OVERFLOW = 2 };
+
+inline uint64_t below(int x) { return x >= 64 ? ~0ull : ((1ull << x) - 1ull); }
+inline uint64_t range(int a, int b) { return a >= b ? 0ull : (below(b) & ~below(a)); }  // [a, b)
+
+// step taken after probe k of a search (lz4.c:896-905 with acceleration 1)
+inline int step_of(int k) { return k == 0 ? 1 : ((64 + k - 1) >> 6); }
+
+// The sequential search loop from probe index b.cnt at position b.ip (strides above 1).
+// Returns true with (P, cand) when a probe verifies; false = last literals.
+bool generic_search(Block &b, int &P, int &cand) {
+  int fwd = b.ip, k = b.cnt;
+  for (;;) {
+    const int cur = fwd;
+    const int nxt = cur + step_of(k);
+    if (nxt > b.mfl1) return false;
+    const uint32_t seq = rd32(b.src + cur);
+    const uint32_t h = hash13(seq);
+    const int m = b.table[h];
+    b.table[h] = uint16_t(cur);
+    if (rd32(b.src + m) == seq) {
+      P = cur;
+      cand = m;
+      return true;
+    }
+    fwd = nxt;
+    ++k;
+  }
+}
+
+inline int ext_bytes(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+
+// One window of 64 positions starting at w0.  Mode says how the walk starts.
+Status window(Block &b, int w0, Mode mode, int forced_cand, Mode &next_mode) {
+  b.windows++;
+  // ---- per-lane precomputation (vector part of the kernel)
+  bool act[64];
+  uint32_t seq[64], h[64];
+  int tc[64], len[64], bkr[64];
+  bool tver[64];
+  uint64_t eq[64];
+  for (int l = 0; l < 64; ++l) {
+    const int i = w0 + l;
+    act[l] = i <= b.n - kMFLimit;
+    seq[l] = 0; h[l] = 0; tc[l] = 0; len[l] = 0; bkr[l] = 0; tver[l] = false;
+    if (!act[l]) continue;
+    seq[l] = rd32(b.src + i);
+    h[l] = hash13(seq[l]);
+    tc[l] = (mode == FORCED && l == 0) ? forced_cand : int(b.table[h[l]]);
+    tver[l] = rd32(b.src + tc[l]) == seq[l];
+    int lim = b.mlim - i;                       // LZ4_count stops at matchlimit
+    if (lim > kRegLen) lim = kRegLen;
+    len[l] = 4 + count_fwd(b, i + 4, tc[l] + 4, lim - 4);
+    int bl = kRegBack;                          // bytes in front of the block do not exist
+    if (bl > tc[l]) bl = tc[l];
+    bkr[l] = count_back(b, i, tc[l], bl);
+  }
+  for (int l = 0; l < 64; ++l) {
+    eq[l] = 0;
+    for (int j = 0; j < 64; ++j)
+      if (act[l] && act[j] && h[j] == h[l]) eq[l] |= 1ull << j;
+  }
+  uint64_t VT = 0, DUP = 0, ACT = 0;
+  for (int l = 0; l < 64; ++l) {
+    if (act[l]) ACT |= 1ull << l;
+    if (tver[l]) VT |= 1ull << l;
+    if (eq[l] & below(l)) DUP |= 1ull << l;
+  }
+  const int NA = ~ACT ? __builtin_ctzll(~ACT) : 64;  // first lane that may not be probed
+
+  // ---- scalar walk
+  const int anchor_in = b.anchor;
+  uint64_t INS = 0, chosen = 0;
+  int L_cand[64], L_len[64], L_bk[64];
+  int anchor = b.anchor, cnt = b.cnt;
+  int q = 0, x = 0, cand = 0, ipn = 0;
+  bool inwin = false;
+  Status st = CONTINUE;
+  next_mode = SEARCH;
+
+  // candidate of lane x given the inserts so far
+  auto lookup = [&](int lx, int &c, bool &iw) -> bool {
+    const uint64_t m = eq[lx] & INS & below(lx);
+    if (m) {
+      const int j = 63 - __builtin_clzll(m);
+      c = w0 + j;
+      iw = true;
+      return seq[j] == seq[lx];
+    }
+    c = tc[lx];
+    iw = false;
+    return (VT >> lx) & 1;
+  };
+
+  // three-state machine, as in the kernel
+  enum { S_SEARCH = 0, S_FOUND = 1, S_POST = 2 };
+  int state = S_SEARCH;
+  if (mode == POSTMATCH) {
+    ipn = w0 + 2;
+    state = S_POST;
+  } else if (mode == FORCED) {
+    x = 0;
+    cand = forced_cand;
+    inwin = false;
+    state = S_FOUND;
+  }
+  for (;;) {
+    if (state == S_SEARCH) {
+      const int xmax = q + (64 - cnt);             // last lane whose probe index is <= 64
+      int stop = NA < 64 ? NA : 64;
+      int why = NA < 64 ? 1 : 0;                   // 1: last literals, 0: window end
+      if (xmax + 1 <= stop) { stop = xmax + 1; why = 2; }  // 2: strides above 1 from here
+      const uint64_t cm = (VT | DUP) & ~below(q) & below(stop);
+      if (!cm) {
+        INS |= range(q, stop);
+        if (why == 1) {
+          st = LAST;
+        } else {
+          b.ip = w0 + stop;
+          b.cnt = cnt + (stop - q);
+        }
+        break;
+      }
+      x = __builtin_ctzll(cm);
+      INS |= range(q, x);
+      const bool ver = lookup(x, cand, inwin);
+      INS |= 1ull << x;
+      cnt += x + 1 - q;
+      q = x + 1;
+      if (ver) state = S_FOUND;
+    } else if (state == S_FOUND) {
+      const int P = w0 + x;
+      int fl, bk;
+      int blim = P - anchor < cand ? P - anchor : cand;
+      if (inwin) {
+        b.inwin++;
+        fl = count_fwd(b, P + 4, cand + 4, b.mlim - (P + 4));
+        bk = count_back(b, P, cand, blim);
+      } else {
+        fl = len[x] - 4;
+        if (len[x] == kRegLen && P + kRegLen < b.mlim) {
+          b.longfwd++;
+          fl += count_fwd(b, P + kRegLen, cand + kRegLen, b.mlim - P - kRegLen);
+        }
+        bk = bkr[x] < blim ? bkr[x] : blim;
+        if (bkr[x] == kRegBack && blim > kRegBack) {
+          b.longback++;
+          bk = kRegBack + count_back(b, P - kRegBack, cand - kRegBack, blim - kRegBack);
+        }
+      }
+      L_cand[x] = cand;
+      L_len[x] = 4 + fl;
+      L_bk[x] = bk;
+      chosen |= 1ull << x;
+      ipn = P + 4 + fl;
+      anchor = ipn;
+      if (ipn >= b.mfl1) { st = LAST; break; }
+      state = S_POST;
+    } else {
+      const int r = ipn - 2 - w0;
+      if (r + 2 >= 64) {  // the re-test position lies beyond this window
+        b.ip = ipn;
+        next_mode = POSTMATCH;
+        break;
+      }
+      INS |= 1ull << r;   // LZ4_putPosition(ip-2), lz4.c:1084
+      x = r + 2;
+      const bool ver = lookup(x, cand, inwin);
+      INS |= 1ull << x;
+      if (ver) {
+        state = S_FOUND;  // immediate match: no literals, no catch-up (anchor == position)
+      } else {
+        q = x + 1;
+        cnt = 0;
+        state = S_SEARCH;
+      }
+    }
+  }
+
+  // ---- table update: every inserted lane, the latest position per hash wins
+  if (st != LAST)
+    for (int l = 0; l < 64; ++l)
+      if (((INS >> l) & 1) && !(eq[l] & INS & ~below(l + 1))) b.table[h[l]] = uint16_t(w0 + l);
+  // ---- emission of the window's sequences, in lane order
+  {
+    int prev = anchor_in, op = b.op;
+    for (int l = 0; l < 64; ++l) {
+      if (!((chosen >> l) & 1)) continue;
+      const int P = w0 + l;
+      const int lit = P - L_bk[l] - prev;
+      const int mc = L_len[l] + L_bk[l] - 4;
+      const int tp = op;
+      // lz4.c:964 and lz4.c:1044 (limitedOutput)
+      if (tp + 1 + lit + (2 + 1 + kLastLiterals) + lit / 255 > b.olimit) return OVERFLOW;
+      const int fp = tp + 1 + ext_bytes(lit) + lit;
+      if (fp + 2 + (1 + kLastLiterals) + (mc + 240) / 255 > b.olimit) return OVERFLOW;
+      b.dst[tp] = uint8_t(((lit < 15 ? lit : 15) << 4) | (mc < 15 ? mc : 15));
+      int o = tp + 1;
+      if (lit >= 15) {
+        int v = lit - 15;
+        for (; v >= 255; v -= 255) b.dst[o++] = 255;
+        b.dst[o++] = uint8_t(v);
+      }
+      memcpy(b.dst + o, b.src + prev, size_t(lit));
+      o += lit;
+      const int off = P - L_cand[l];
+      b.dst[o++] = uint8_t(off);
+      b.dst[o++] = uint8_t(off >> 8);
+      if (mc >= 15) {
+        int v = mc - 15;
+        for (; v >= 255; v -= 255) b.dst[o++] = 255;
+        b.dst[o++] = uint8_t(v);
+      }
+      op = o;
+      prev = P + L_len[l];
+    }
+    b.op = op;
+  }
+  b.anchor = anchor;
+  return st;
+}
+
+}  // namespace
+
+extern "C" int sim_lz4_window_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap,
+                                    long *stats /* 5 counters, may be null */) {
+  static thread_local Block b;
+  b.src = src;
+  b.n = n;
+  b.dst = dst;
+  b.mfl1 = n - kMFLimit + 1;
+  b.mlim = n - kLastLiterals;
+  b.olimit = dst_cap;
+  b.ip = 1; b.cnt = 0; b.anchor = 0; b.op = 0;
+  b.windows = b.generic = b.inwin = b.longfwd = b.longback = 0;
+  memset(b.table, 0, sizeof b.table);
+  if (n >= kMFLimit + 1) {  // LZ4_minLength (lz4.c:876)
+    Mode mode = SEARCH;
+    int forced = 0;
+    for (;;) {
+      int w0;
+      if (mode == SEARCH && b.cnt > 64) {
+        b.generic++;
+        int P, cand;
+        if (!generic_search(b, P, cand)) break;
+        mode = FORCED;
+        forced = cand;
+        w0 = P;
+      } else {
+        w0 = mode == POSTMATCH ? b.ip - 2 : b.ip;
+      }
+      Mode nm;
+      const Status st = window(b, w0, mode, forced, nm);
+      if (st == OVERFLOW) return 0;
+      if (st == LAST) break;
+      mode = nm;
+    }
+  }
+  // last literals (lz4.c:1141-1166)
+  const int lastRun = n - b.anchor;
+  if (b.op + lastRun + 1 + (lastRun + 255 - 15) / 255 > b.olimit) return 0;
+  int op = b.op;
+  if (lastRun >= 15) {
+    int acc = lastRun - 15;
+    dst[op++] = 15 << 4;
+    for (; acc >= 255; acc -= 255) dst[op++] = 255;
+    dst[op++] = uint8_t(acc);
+  } else {
+    dst[op++] = uint8_t(lastRun << 4);
+  }
+  memcpy(dst + op, src + b.anchor, size_t(lastRun));
+  op += lastRun;
+  if (stats) {
+    stats[0] = b.windows; stats[1] = b.generic; stats[2] = b.inwin;
+    stats[3] = b.longfwd; stats[4] = b.longback;
+  }
+  return op;
+}

@@ -326,3 +326,29 @@ def test_fast_compress_ratio_within_5pct(engine, oracle_mod):
 def test_fast_compress_deterministic(engine):
     inputs = _fast_inputs(44, 8)
     assert _fast_compress(engine, inputs) == _fast_compress(engine, inputs)
+
+
+def test_batch_compress_window_engine_inputs(engine, oracle_mod):
+    """The inputs that drive every path of the windowed exact engine (in-window
+    candidates, matches and catch-ups longer than the register windows, searches that
+    outlast the stride-1 probes, window hand-over after a match, stored blocks): frames
+    byte-identical to the oracle's, as one batch."""
+    import torch
+    from test_window_sim import _inputs
+    inputs = _inputs(1, 250)
+    inputs += [b"".join(inputs[i] for i in range(k, k + 9)) for k in range(0, 90, 9)]  # multi-block
+    hbuf, hoffs = _pack(inputs)
+    d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
+    in_offs = torch.tensor(hoffs, dtype=torch.int64, device="cuda")
+    in_lens = torch.tensor([len(b) for b in inputs], dtype=torch.int32, device="cuda")
+    bounds = [(engine.lz4f_compress_bound(len(b)) + 63) // 64 * 64 for b in inputs]
+    ooffs = np.concatenate([[0], np.cumsum(bounds)[:-1]])
+    d_out = torch.empty(int(sum(bounds)) + 256, dtype=torch.uint8, device="cuda")
+    out_offs = torch.tensor(ooffs, dtype=torch.int64, device="cuda")
+    out_lens = torch.zeros(len(inputs), dtype=torch.int32, device="cuda")
+    engine.lz4f_compress_batch(d_in, in_offs, in_lens, d_out, out_offs, out_lens)
+    host_out = bytes(d_out.cpu().numpy())
+    flens = out_lens.cpu().numpy()
+    for i, b in enumerate(inputs):
+        fr = host_out[ooffs[i]:ooffs[i] + flens[i]]
+        assert fr == oracle_mod.rdk_lz4_compress(b)[1], (i, len(b))

@@ -194,6 +194,25 @@ int rdk_hip_lz4f_decompress(const void *d_in, const uint64_t *d_in_offs,
                             uint32_t *d_out_lens, int32_t *d_status, uint32_t n,
                             void *stream);
 
+/* rdk_hip_lz4f_decompress for callers that cannot allocate (code under HIP
+ * graph capture, tight serving loops, harnesses that forbid hipMalloc).  It has
+ * no counterpart in the reference.  Same arguments and results; the frame and
+ * block descriptor tables live in a fixed device array that is part of the
+ * library (about 1.9 MB on every GPU the library is initialised on, held until
+ * the process ends) instead of the per-thread scratch the plain entry point
+ * grows on demand.  The call allocates and frees nothing and clears its work
+ * counter with a kernel, not a memset.  rdk_hip_init(device) must have run for
+ * the current device (it looks the array's address up); n is limited to
+ * RDK_HIP_LZ4F_NOALLOC_MAX_FRAMES (RDK_HIP_E_INVAL beyond).  Every call on a GPU
+ * shares that GPU's array: calls that overlap in time on one GPU race, so keep
+ * them on one stream or order them yourself. */
+#define RDK_HIP_LZ4F_NOALLOC_MAX_FRAMES 1024u
+int rdk_hip_lz4f_decompress_noalloc(const void *d_in, const uint64_t *d_in_offs,
+                                    const uint32_t *d_in_lens, void *d_out,
+                                    const uint64_t *d_out_offs, const uint32_t *d_out_caps,
+                                    uint32_t *d_out_lens, int32_t *d_status, uint32_t n,
+                                    void *stream);
+
 /* ---------------------------------------------------------------------------
  * Producer batching front-end (north_star).  One
  * producer per broker thread: a ring of `nslots` pinned host staging slots,

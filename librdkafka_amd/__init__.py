@@ -51,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "rdk_hip_producer_flush", "rdk_hip_producer_poll", "rdk_hip_producer_destroy",
     "rdk_hip_gen_json", "rdk_hip_msgset_v2_sizes", "rdk_hip_msgset_v2_write",
     "rdk_hip_msgset_v2_index", "rd_slice_crc32", "rdk_hip_crc32_ranges",
-    "rdk_hip_msgset_v01_crc",
+    "rdk_hip_msgset_v01_crc", "rdk_hip_lz4f_decompress_noalloc",
 )
 
 
@@ -109,6 +109,8 @@ def lib():
         L.rdk_hip_lz4f_compress_fast.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp]
         L.rdk_hip_lz4f_decompress.restype = i32
         L.rdk_hip_lz4f_decompress.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
+        L.rdk_hip_lz4f_decompress_noalloc.restype = i32
+        L.rdk_hip_lz4f_decompress_noalloc.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
     L.rdk_hip_producer_new.restype = vp
     L.rdk_hip_producer_new.argtypes = [i32, sz, i32, i32]
     L.rdk_hip_producer_produce.restype = i32
@@ -364,6 +366,20 @@ def lz4f_decompress_batch(src, in_offs, in_lens, dst, out_offs, out_caps, out_le
                                          _ptr(out_offs), _ptr(out_caps), _ptr(out_lens),
                                          _ptr(status), int(in_offs.numel()), _stream(stream)),
            "lz4f_decompress")
+
+
+LZ4F_NOALLOC_MAX_FRAMES = 1024
+
+
+def lz4f_decompress_batch_noalloc(src, in_offs, in_lens, dst, out_offs, out_caps, out_lens,
+                                  status, stream=None):
+    """rdk_hip_lz4f_decompress_noalloc: the batch decoder on the library's fixed device
+    scratch (no allocation; at most LZ4F_NOALLOC_MAX_FRAMES frames; init() first)."""
+    _check(lib().rdk_hip_lz4f_decompress_noalloc(_ptr(src), _ptr(in_offs), _ptr(in_lens),
+                                                 _ptr(dst), _ptr(out_offs), _ptr(out_caps),
+                                                 _ptr(out_lens), _ptr(status),
+                                                 int(in_offs.numel()), _stream(stream)),
+           "lz4f_decompress_noalloc")
 
 
 PRODUCER_EXACT, PRODUCER_FAST = 0, 1

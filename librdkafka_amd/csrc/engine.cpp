@@ -17,6 +17,8 @@
 
 namespace rdk {
 
+int lz4f_noalloc_setup(int dev);  // lz4_decode.hip: per-device address of its static scratch
+
 static thread_local char tl_err[512];
 static thread_local Ctx *tl_ctx = nullptr;
 
@@ -95,6 +97,7 @@ int bind(int dev) {
   RDK_HIP_CHECK(hipSetDevice(dev));
   int rc = upload_tables(dev);
   if (rc) return rc;
+  if ((rc = lz4f_noalloc_setup(dev))) return rc;
   if (!tl_ctx) tl_ctx = new Ctx();
   if (tl_ctx->device != dev) {
     if (tl_ctx->stream) (void)hipStreamDestroy(tl_ctx->stream);

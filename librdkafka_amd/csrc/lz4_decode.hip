@@ -681,9 +681,71 @@ void launch_decode(uint8_t *scratch, const uint8_t *d_in, const uint64_t *d_in_o
                      d_out_offs, n, fs, bd, d_out_lens, d_status);
 }
 
+// ------------------------------------------------ allocation-free variant
+// The same four kernels on a scratch buffer that is part of the code object, for callers
+// that cannot allocate (HIP graph capture, tight serving loops).  One array per GPU, held
+// until the process ends; every call on a GPU shares it, so calls that overlap on one GPU
+// race.  The host never passes the array's name to a kernel: its per-device address is
+// looked up once, at rdk_hip_init(), and that pointer is what the launches use.
+constexpr size_t noalloc_scratch_bytes(uint32_t n) {
+  return ((size_t(n) * sizeof(FrameState) + 255) & ~size_t(255)) +
+         size_t(n) * kMaxDesc * sizeof(BlockDesc) + 256 + size_t(n) * kMaxDesc * sizeof(uint32_t);
+}
+constexpr size_t kNoAllocBytes = noalloc_scratch_bytes(RDK_HIP_LZ4F_NOALLOC_MAX_FRAMES);
+static_assert(kNoAllocBytes <= (4u << 20), "the static scratch is meant to stay modest");
+static __device__ __align__(256) uint8_t scratch[kNoAllocBytes];
+
+namespace {
+constexpr int kNoAllocMaxDev = 64;
+uint8_t *g_noalloc_ptr[kNoAllocMaxDev];  // per device: that GPU's copy of `scratch`
+}  // namespace
+
+// Called by rdk_hip_init() with `dev` current.
+int lz4f_noalloc_setup(int dev) {
+  if (dev < 0 || dev >= kNoAllocMaxDev) return set_error(RDK_HIP_E_INVAL, "device %d", dev);
+  if (__atomic_load_n(&g_noalloc_ptr[dev], __ATOMIC_ACQUIRE)) return 0;
+  uint8_t *ptr = nullptr;
+  RDK_HIP_CHECK(hipGetSymbolAddress(reinterpret_cast<void **>(&ptr), HIP_SYMBOL(scratch)));
+  if (!ptr) return set_error(RDK_HIP_E_HIP, "hipGetSymbolAddress(scratch) returned null");
+  __atomic_store_n(&g_noalloc_ptr[dev], ptr, __ATOMIC_RELEASE);
+  return 0;
+}
+
+// a kernel, not hipMemsetAsync: the call may be recorded into a HIP graph
+__global__ void lz4f_zero_word_kernel(uint32_t *p) { *p = 0u; }
+
 }  // namespace rdk
 
 using namespace rdk;
+
+RDK_API int rdk_hip_lz4f_decompress_noalloc(const void *d_in, const uint64_t *d_in_offs,
+                                            const uint32_t *d_in_lens, void *d_out,
+                                            const uint64_t *d_out_offs,
+                                            const uint32_t *d_out_caps, uint32_t *d_out_lens,
+                                            int32_t *d_status, uint32_t n, void *stream) {
+  if (!n) return RDK_HIP_OK;
+  if (n > RDK_HIP_LZ4F_NOALLOC_MAX_FRAMES)
+    return set_error(RDK_HIP_E_INVAL, "%u frames exceed RDK_HIP_LZ4F_NOALLOC_MAX_FRAMES (%u)", n,
+                     unsigned(RDK_HIP_LZ4F_NOALLOC_MAX_FRAMES));
+  if (!d_in || !d_in_offs || !d_in_lens || !d_out || !d_out_offs || !d_out_caps || !d_out_lens ||
+      !d_status)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  int dev = -1;
+  RDK_HIP_CHECK(hipGetDevice(&dev));
+  uint8_t *ptr = (dev >= 0 && dev < kNoAllocMaxDev)
+                     ? __atomic_load_n(&g_noalloc_ptr[dev], __ATOMIC_ACQUIRE) : nullptr;
+  if (!ptr)
+    return set_error(RDK_HIP_E_INVAL, "rdk_hip_init(%d) has not run: no scratch address for this device", dev);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // the work counter sits behind the FrameState and BlockDesc tables of THIS call's n
+  const size_t counter_at = noalloc_scratch_bytes(n) - 256 - size_t(n) * kMaxDesc * sizeof(uint32_t);
+  hipLaunchKernelGGL(lz4f_zero_word_kernel, dim3(1), dim3(1), 0, s,
+                     reinterpret_cast<uint32_t *>(ptr + counter_at));
+  launch_decode(ptr, static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
+                static_cast<uint8_t *>(d_out), d_out_offs, d_out_caps, d_out_lens, d_status, n, s);
+  RDK_HIP_CHECK(hipGetLastError());
+  return RDK_HIP_OK;
+}
 
 RDK_API int rdk_hip_lz4f_decompress(const void *d_in, const uint64_t *d_in_offs,
                                     const uint32_t *d_in_lens, void *d_out,

@@ -1,16 +1,20 @@
 #!/usr/bin/env python3
 """bench.py -- librdkafka record-batch engine on MI355X.
 
-Headline (BASELINE.json configs[1]): CRC32C over 1M synthetic MsgVersion 2
-record batches of 16 KiB on one MI355X, device-resident, bit-exact with
-crc32c.c.  One step = one pass of the hot path (rd_kafka_msgset_writer
-CRC finalize, rdkafka_msgset_writer.c:1229-1246) over all batches.
+Headline = BASELINE.json's metric itself, "record-batch GB/s (CRC32C+LZ4F)": the writer's
+finalize of device-resident MsgVersion 2 MessageSets (rd_kafka_msgset_writer_finalize,
+rdkafka_msgset_writer.c:1335: LZ4F compress :1128-1221 with frames byte-identical to
+rd_kafka_lz4_compress, header finalize :1251-1295, CRC32C :1229-1246) over `--partitions`
+toppars per GPU, each with one linger-accumulated 1 MiB batch of JSON records
+(configs[2] input, configs[4] shape).  One step = one rdk_hip_msgset_v2_finalize call over
+all batches; value = uncompressed record bytes per second.  configs[1] (CRC32C only over
+1M x 16 KiB batches) and the other configs are `legs` of the same JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload crc|lz4c|lz4d|consumer]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ...]
 
-For N>1 it is launched by torch.distributed.run, one rank per GPU.  Batches
-shard by topic-partition across GPUs with no data-path collective (weak
-scaling); gloo carries only the barrier and the max-over-ranks time.
+--gpus N started by hand launches N ranks itself (torch.distributed.run); under a launcher
+it checks WORLD_SIZE.  Batches shard by topic-partition across GPUs with no data-path
+collective (weak scaling); gloo carries only the barrier and the max-over-ranks time.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -29,6 +33,44 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CRC_BATCHES = 1 << 20          # configs[1]: 1M batches
 CRC_BATCH_BYTES = 16384        # of 16 KiB
 CPU_THREADS = 16               # the GPU box's CPU share per GPU
+
+
+def source_hash() -> str:
+    """sha256 over the kernel sources the library is built from: ties a profile summary
+    under profiles/ to the build that bench.py is timing."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(ROOT, "librdkafka_amd", "csrc")
+    for f in sorted(os.listdir(d)) + ["../Makefile"]:
+        with open(os.path.join(d, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+
+
+def profile_summary(leg: str, alg_bytes: int, kernel_ms: float):
+    """(traffic_bytes, note) from profiles/r02/<leg>.json -- the rocprofv3 summary of this leg
+    (scripts/profile_r2.sh) -- only when it was taken from the same kernel sources and the
+    same algorithmic bytes; its kernel-trace average must agree with the HIP-event time."""
+    path = os.path.join(PROFILE_DIR, leg + ".json")
+    try:
+        with open(path) as f:
+            p = json.load(f)
+    except (OSError, ValueError):
+        return None, {"profile": None}
+    note = {"profile": os.path.relpath(path, ROOT), "profile_source_hash": p.get("source_hash"),
+            "profile_kernel_ms": round(p["avg_ns"] / 1e6, 4) if p.get("avg_ns") else None}
+    if p.get("source_hash") != source_hash():
+        note["profile_stale"] = "kernel sources changed since the profile was taken"
+        return None, note
+    if int(p.get("alg_bytes_per_launch", -1)) != int(alg_bytes):
+        note["profile_stale"] = "different workload (algorithmic bytes differ)"
+        return None, note
+    if p.get("avg_ns") and kernel_ms:
+        note["profile_vs_events"] = round(p["avg_ns"] / 1e6 / kernel_ms, 4)
+    return (int(p["traffic_bytes"]) if "traffic_bytes" in p else None), note
 
 
 def shard_partitions(n_partitions: int, rank: int, world: int) -> list[int]:
@@ -167,6 +209,84 @@ def json_batches(n, size=JSON_BATCH, seed=42):
     return buf, offs, lens
 
 
+def json_msgsets(n, size=JSON_BATCH, seed=42):
+    """n device-resident MessageSets as the writer leaves them before finalize: a 61-byte v2
+    header directly followed by `size` bytes of JSON records (8 distinct MiB rotated)."""
+    import numpy as np
+    import torch
+    import librdkafka_amd as L
+    from librdkafka_amd import workload as W
+    distinct = 8
+    host = L.gen_json(size * distinct, seed)
+    base = torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda()
+    stride = (61 + size + 255) // 256 * 256
+    buf = torch.zeros(n * stride + 256, dtype=torch.uint8, device="cuda")
+    hdrs = torch.frombuffer(bytearray(b"".join(W.v2_header(i, 61 + size) for i in range(n))),
+                            dtype=torch.uint8).cuda().view(n, 61)
+    v = buf[:n * stride].view(n, stride)
+    v[:, :61] = hdrs
+    for i in range(n):
+        j = i % distinct
+        v[i, 61:61 + size] = base[j * size:(j + 1) * size]
+    rec_offs = torch.arange(n, dtype=torch.int64, device="cuda") * stride + 61
+    rec_lens = torch.full((n,), size, dtype=torch.int32, device="cuda")
+    del np
+    return buf, rec_offs, rec_lens
+
+
+def bench_finalize(args, rank, world, n=None, mode=0):
+    """The headline step: rdk_hip_msgset_v2_finalize (LZ4F compress + v2 header finalize +
+    CRC32C finalize, rdkafka_msgset_writer.c:1335) over n device-resident 1 MiB MessageSets.
+    mode 0 = frames byte-identical to rd_kafka_lz4_compress, 1 = the throughput compressor.
+    Also times the compress stage alone (its two kernels) for the roofline of the dominant
+    kernel, and checks the finished batches on the device: CRC VERIFY all zero, every frame
+    decompressed by the engine equals its records."""
+    import torch
+    import librdkafka_amd as L
+    n = n or args.partitions
+    src, rec_offs, rec_lens = json_msgsets(n, seed=42 + rank)
+    cap = (61 + L.lz4f_compress_bound(JSON_BATCH) + 255) // 256 * 256
+    dst = torch.empty(n * cap + 256, dtype=torch.uint8, device="cuda")
+    out_offs = torch.arange(n, dtype=torch.int64, device="cuda") * cap
+    out_caps = torch.full((n,), cap, dtype=torch.int32, device="cuda")
+    flens, blens, crcs = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+
+    def step():
+        L.msgset_v2_finalize(src, rec_offs, rec_lens, dst, out_offs, out_caps, flens, blens, crcs,
+                             mode=mode)
+
+    ms, kms = _timed(step, args.steps, args.warmup, world)
+    # the compress stage alone, same inputs and outputs (block kernel + frame assembly)
+    frame_offs = out_offs + 61
+    comp = L.lz4f_compress_fast_batch if mode else L.lz4f_compress_batch
+    _, comp_kms = _timed(lambda: comp(src, rec_offs, rec_lens, dst, frame_offs, flens),
+                         max(3, args.steps // 2), 1, 1)
+    step()
+    # correctness gate on the timed configuration
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    L.msgset_v2_crc(dst, out_offs, out_caps, st, L.V2_CRC_VERIFY)
+    if int(st.abs().sum()):
+        raise SystemExit(f"rank {rank}: CRC verify failures in the finished batches")
+    dec = torch.empty(n * JSON_BATCH + 256, dtype=torch.uint8, device="cuda")
+    doffs = torch.arange(n, dtype=torch.int64, device="cuda") * JSON_BATCH
+    dcaps = torch.full((n,), JSON_BATCH, dtype=torch.int32, device="cuda")
+    dl = torch.zeros(n, dtype=torch.int32, device="cuda")
+    L.lz4f_decompress_batch(dst, frame_offs, flens, dec, doffs, dcaps, dl, st)
+    stride = (61 + JSON_BATCH + 255) // 256 * 256
+    recs = src[:n * stride].view(n, stride)[:, 61:61 + JSON_BATCH]
+    if int(st.abs().sum()) or not bool((dl == JSON_BATCH).all()) or \
+            not torch.equal(dec[:n * JSON_BATCH].view(n, JSON_BATCH), recs):
+        raise SystemExit(f"rank {rank}: finished frames do not decompress to their records")
+    if not bool((blens == flens + 61).all()):
+        raise SystemExit(f"rank {rank}: a JSON batch was left uncompressed")
+    clen = int(flens.to(torch.int64).sum())
+    nbytes = n * JSON_BATCH
+    return {"ms": ms, "kernel_ms": kms, "comp_kernel_ms": comp_kms, "bytes": nbytes, "records": n,
+            # step: records read + frame written (compress), frame re-read + 4 B (CRC), header
+            "alg_bytes": nbytes + clen + clen + 61 * n,
+            "comp_alg_bytes": nbytes + clen, "ratio": nbytes / clen}
+
+
 def bench_lz4c(args, rank, world, n=None, fast=False, level=0):
     """configs[2]: LZ4F compress (rd_kafka_lz4_compress semantics) of 1 MiB
     JSON batches.  fast=False: frames byte-identical to the reference's;
@@ -174,7 +294,7 @@ def bench_lz4c(args, rank, world, n=None, fast=False, level=0):
     within 5 % of the reference's)."""
     import torch
     import librdkafka_amd as L
-    n = n or args.partitions // world
+    n = n or args.partitions
     src, offs, lens = json_batches(n, seed=42 + rank)
     bound = (L.lz4f_compress_bound(JSON_BATCH) + 255) // 256 * 256
     dst = torch.empty(n * bound + 256, dtype=torch.uint8, device="cuda")
@@ -200,8 +320,8 @@ def bench_consumer(args, rank, world, n=None):
     import torch
     import librdkafka_amd as L
     from librdkafka_amd import workload as W
-    n = n or args.partitions // world
-    c = bench_lz4c(argparse.Namespace(steps=1, warmup=0, partitions=n * world), rank, world, n)
+    n = n or args.partitions
+    c = bench_lz4c(argparse.Namespace(steps=1, warmup=0, partitions=n), rank, world, n)
     frames, foffs, flens = c["frames"]
     fl = flens.cpu().numpy().astype(np.int64)
     slot = (61 + int(fl.max()) + 255) // 256 * 256
@@ -278,7 +398,7 @@ def bench_serialize(args, rank, world, n=None, per_batch=9500):
     import numpy as np
     import torch
     import librdkafka_amd as L
-    n = n or args.partitions // world
+    n = n or args.partitions
     base, d, payload = tiled_messages(n, per_batch, seed=42 + rank)
     b = np.zeros(n, dtype=L.V2_BATCH_DTYPE)
     b["first_msg"] = np.arange(n) * per_batch
@@ -319,7 +439,7 @@ def bench_index(args, rank, world, n=None, per_batch=9500):
     import numpy as np
     import torch
     import librdkafka_amd as L
-    n = n or args.partitions // world
+    n = n or args.partitions
     base, d, _ = tiled_messages(n, per_batch, seed=42 + rank)
     b = np.zeros(n, dtype=L.V2_BATCH_DTYPE)
     b["first_msg"] = np.arange(n) * per_batch
@@ -351,7 +471,7 @@ def bench_legacy(args, rank, world, n=None, set_bytes=1 << 20):
     import torch
     import librdkafka_amd as L
     from librdkafka_amd import workload as W
-    n = n or args.partitions // world
+    n = n or args.partitions
     base = W.gen_messages(16384, seed=42 + rank)
     one = W.msgset_v01_bytes(base, 0, 16384, magic=1, max_bytes=set_bytes)
     msgs = 0
@@ -455,11 +575,11 @@ def bench_producer(args, rank, world, n=None, threads=None, mode=1, slot_mib=Non
     import numpy as np
     import librdkafka_amd as L
     from librdkafka_amd import workload as W
-    n = n or args.partitions // world
-    # measured sweep (threads x slot MiB): 1x256 17, 2x128 20.3, 2x64 18.7, 4x64 16.2,
-    # 4x128 14.7, 8x16 11.6 GB/s -- host gather + PCIe bound, more streams than
-    # the 4 hardware queues serialise the compress launches
-    threads = threads or int(os.environ.get("RDK_BENCH_PRODUCER_THREADS", "2"))
+    n = n or args.partitions
+    # measured sweep (threads x slot MiB, 4 slots each): 1x32 18.5, 1x64 22.2, 1x128 27.4,
+    # 2x64 26.5, 2x128 9.6, 1x256 5.8 GB/s -- host gather + PCIe bound; past ~1 GiB of pinned
+    # staging in the rings the host-side gather slows down sharply on this box
+    threads = threads or int(os.environ.get("RDK_BENCH_PRODUCER_THREADS", "1"))
     slot_mib = slot_mib or int(os.environ.get("RDK_BENCH_PRODUCER_SLOT_MIB", "128"))
     distinct = 8
     recs = [L.gen_json(JSON_BATCH, 42 + rank * 97 + j) for j in range(distinct)]
@@ -491,7 +611,8 @@ def bench_producer(args, rank, world, n=None, threads=None, mode=1, slot_mib=Non
         for th in ths:
             th.join()
 
-    once()  # warm-up: staging allocations, first-touch of pinned memory
+    once()  # warm-up: staging allocations, first touch of every slot's pinned memory
+    once()
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -596,13 +717,145 @@ def cpu_baseline_lz4(kind, n=64, seconds=4.0, level=0):
                       f"{cpu_model()}"}
 
 
+def cpu_reference_lz4(kind, n=64, seconds=4.0, level=0, with_crc=False):
+    """The reference's own compiled lz4frame.c / lz4.c / lz4hc.c (oracle/_ref, built from
+    /root/reference/src in the build container), driven like rd_kafka_lz4_compress /
+    _decompress (rdkafka_lz4.c:329-442 / :167-317: fresh LZ4F context and malloc per call),
+    on CPU_THREADS host threads over n x 1 MiB JSON batches.  with_crc adds the CRC32C pass
+    of calc_crc_v2 over the frames (crc32c_hw restated: crc32c.c itself needs the generated
+    config.h).  Falls back to the restatement (kind "port") when the reference build is not
+    in the tree."""
+    import numpy as np
+    import oracle
+    import librdkafka_amd as L
+    R = oracle.ref()
+    if R is None:
+        return cpu_baseline_lz4(kind, n, seconds, level)
+    data = np.frombuffer(L.gen_json(JSON_BATCH * 8, 42), dtype=np.uint8)
+    src = np.concatenate([data] * (n // 8))
+    offs = (np.arange(n, dtype=np.uint64) * JSON_BATCH).astype(np.uint64)
+    lens = np.full(n, JSON_BATCH, dtype=np.uint32)
+    bound = int(oracle.lib().or_lz4f_compress_bound(JSON_BATCH))
+    cbuf = np.zeros(n * bound, dtype=np.uint8)
+    coffs = (np.arange(n, dtype=np.uint64) * bound).astype(np.uint64)
+    clens = np.zeros(n, dtype=np.uint32)
+    crcs = np.zeros(n, dtype=np.uint32)
+    lib = oracle.lib()
+
+    def comp():
+        assert R.ref_lz4f_compress_batches_mt(src.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                              n, cbuf.ctypes.data, coffs.ctypes.data,
+                                              clens.ctypes.data, level, CPU_THREADS) == 0
+        if with_crc:
+            lib.or_crc32c_batches_mt(cbuf.ctypes.data, coffs.ctypes.data, clens.ctypes.data,
+                                     crcs.ctypes.data, n, CPU_THREADS)
+
+    comp()
+    dbuf = np.zeros(n * JSON_BATCH, dtype=np.uint8)
+    dlens = np.zeros(n, dtype=np.uint32)
+
+    def dec():
+        if with_crc:
+            lib.or_crc32c_batches_mt(cbuf.ctypes.data, coffs.ctypes.data, clens.ctypes.data,
+                                     crcs.ctypes.data, n, CPU_THREADS)
+        assert R.ref_lz4f_decompress_batches_mt(cbuf.ctypes.data, coffs.ctypes.data,
+                                                clens.ctypes.data, n, 1 << 30, dbuf.ctypes.data,
+                                                offs.ctypes.data, dlens.ctypes.data,
+                                                CPU_THREADS) == 0
+
+    fn = comp if kind == "compress" else dec
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    what = f"rd_kafka_lz4_{kind} driven through the reference's compiled lz4frame.c"
+    if level:
+        what += f" at compression.level {level}"
+    if with_crc:
+        what += " + CRC32C of the frames (crc32c_hw restated)"
+    return {"value": round(passes * n * JSON_BATCH / el / 1e9, 3), "unit": "GB/s",
+            "cores": CPU_THREADS, "kind": "reference",
+            "sample": f"{n} x 1 MiB JSON batches, {passes} passes, {what}, {cpu_model()}"}
+
+
+def bench_dropin_calls(seconds=0.4):
+    """Per-call cost of the drop-in symbols (host buffer in, host result out: gather into
+    pinned staging, H2D, kernels, D2H, stream synchronise) at the reference's batch sizes,
+    beside the reference's compiled code on one host core.  Microseconds per call."""
+    import ctypes as C
+    import numpy as np
+    import oracle
+    import librdkafka_amd as L
+    lib, olib, R = L.lib(), oracle.lib(), oracle.ref()
+    out = {}
+
+    def per_call(fn):
+        fn()
+        calls, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            calls += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return round(el / calls * 1e6, 1)
+
+    for size in (16384, 65536, 1 << 20):
+        data = L.gen_json(size, 7)
+        buf = C.create_string_buffer(data, size)
+        row = {}
+        row["crc32c_gpu_us"] = per_call(lambda: lib.crc32c(0, buf, size))
+        row["crc32c_cpu_us"] = per_call(lambda: olib.or_crc32c_hw(0, buf, size))
+        segs = [data[:61], data[61:]]
+        sl = L.RdSlice(segs)
+
+        def slice_crc():
+            sl.slice.seg = C.pointer(sl._segs[0])
+            sl.slice.rof = 0
+            return lib.rd_slice_crc32c(sl.ptr)
+        row["rd_slice_crc32c_gpu_us"] = per_call(slice_crc)
+        err, frame = L.rd_kafka_lz4_compress(1, 0, data)
+        assert err == 0
+        row["lz4_compress_gpu_us"] = per_call(lambda: L.rd_kafka_lz4_compress(1, 0, data))
+        row["lz4_decompress_gpu_us"] = per_call(lambda: L.rd_kafka_lz4_decompress(1, 0, frame))
+        if R is not None:
+            seg = C.c_char_p(data)
+            sl1 = C.c_size_t(size)
+            o, ol, g = C.c_void_p(), C.c_size_t(), C.c_int()
+
+            def ref_c():
+                assert R.ref_rdk_lz4_compress(1, 0, C.byref(seg), C.byref(sl1), 1, C.byref(o),
+                                              C.byref(ol)) == 0
+                R.ref_free(o)
+            fbuf = C.create_string_buffer(frame, len(frame))
+
+            def ref_d():
+                assert R.ref_rdk_lz4_decompress(1, fbuf, len(frame), 1 << 30, C.byref(o),
+                                                C.byref(ol), C.byref(g)) == 0
+                R.ref_free(o)
+            row["lz4_compress_cpu_us"] = per_call(ref_c)
+            row["lz4_decompress_cpu_us"] = per_call(ref_d)
+        out[f"{size}B"] = row
+    del np
+    out["note"] = ("gpu: drop-in symbol through the C ABI on a host buffer (PCIe round trip + "
+                   "synchronise per call, includes the Python/ctypes call overhead of ~1-3 us); "
+                   "cpu: the reference's compiled lz4frame.c (kind reference) and crc32c_hw "
+                   "restated (port), one core, " + cpu_model())
+    return out
+
+
 def leg_line(name, res, steps, world, cpu=None):
     d = {"GB_per_s": round(res["bytes"] * world / (res["ms"] / 1e3) / 1e9, 2),
          "ms_per_step": round(res["ms"], 3), "batches": res["records"] * world}
     if res.get("kernel_ms"):
         ach = res["alg_bytes"] / (res["kernel_ms"] / 1e3) / 1e9
+        traffic, note = profile_summary(name, res["alg_bytes"], res["kernel_ms"])
         d["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel_ms": round(res["kernel_ms"], 4),
+                         "alg_bytes_per_launch": int(res["alg_bytes"]), **note}
     if "out_bytes" in res:
         d["compression_ratio"] = round(res["bytes"] / max(1, res["out_bytes"]), 3)
         d["pcie_inclusive"] = True
@@ -618,14 +871,14 @@ def index_leg(rank, world, no_cpu):
     res = bench_index(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
     cpu = None if no_cpu else cpu_baseline_index(*res.pop("host_sample"))
     res.pop("host_sample", None)
-    return leg_line("index", res, 3, world, cpu)
+    return leg_line("v2_record_index_1MiB_json", res, 3, world, cpu)
 
 
 def legacy_leg(rank, world, no_cpu):
     res = bench_legacy(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
     cpu = None if no_cpu else cpu_baseline_legacy(*res.pop("host_sample"))
     res.pop("host_sample", None)
-    d = leg_line("legacy", res, 3, world, cpu)
+    d = leg_line("v1_msgset_crc32_verify_1MiB_json", res, 3, world, cpu)
     d["finalize_kernel_ms"] = res["finalize_kernel_ms"]
     return d
 
@@ -634,41 +887,38 @@ def serialize_leg(rank, world, no_cpu):
     res = bench_serialize(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
     cpu = None if no_cpu else cpu_baseline_serialize(*res.pop("host_sample"))
     res.pop("host_sample", None)
-    return leg_line("serialize", res, 3, world, cpu)
-
-
-# HBM bytes per launch from rocprofv3 PMC passes on this kernel and workload
-# (scripts/profile_crc.sh -> scripts/pmc_summary.py; FETCH_SIZE x2 on gfx950).
-# Counters cannot be read in-process, so the committed summary of the same
-# kernel build and batch shape is used; null when they do not match.
-CRC_VARIANT = "v1" if os.environ.get("RDK_HIP_CRC_V1") else "v" + os.environ.get("RDK_HIP_CRC_V", "4")
-CRC_KERNEL = ("crc32c_msgset_v2_v4_kernel<FINALIZE>" if CRC_VARIANT == "v4"
-              else "crc32c_msgset_v2_kernel<%d, FINALIZE>" % int(CRC_VARIANT[1:]))
-CRC_PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_crc_%s" % CRC_VARIANT, "summary.json")
-
-
-def pmc_traffic(path, alg_bytes):
-    try:
-        with open(path) as f:
-            s = json.load(f)
-    except (OSError, ValueError):
-        return None, None
-    if int(s.get("alg_bytes_per_launch", -1)) != int(alg_bytes) or "traffic_bytes" not in s:
-        return None, None
-    return int(s["traffic_bytes"]), os.path.relpath(path, ROOT)
+    return leg_line("v2_record_serialize_1MiB_json", res, 3, world, cpu)
 
 
 # ------------------------------------------------------------------ main
+def crc_leg(args, rank, world):
+    """configs[1]: CRC32C only, 1M x 16 KiB MsgVersion 2 batches (writer finalize)."""
+    res = bench_crc(args, rank, world)
+    ms = res["wall_s"] * 1e3 / args.steps
+    achieved = res["alg_bytes"] / (res["kernel_ms"] / 1e3) / 1e9
+    traffic, note = profile_summary("crc32c_only_16KiB_batches", res["alg_bytes"], res["kernel_ms"])
+    d = {"GB_per_s": round(res["bytes"] / (ms / 1e3) / 1e9, 2), "ms_per_step": round(ms, 4),
+         "batches": res["records"], "batch_bytes": CRC_BATCH_BYTES,
+         "msgs_per_s": round(res["records"] / (ms / 1e3), 1),
+         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                      "kernel": "crc32c_msgset_v2_v4_kernel<FINALIZE>",
+                      "kernel_ms": round(res["kernel_ms"], 4),
+                      "alg_bytes_per_launch": int(res["alg_bytes"]), **note}}
+    return d, res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="crc",
-                    choices=["crc", "lz4c", "lz4c_fast", "lz4hc", "consumer", "producer", "serialize",
-                             "index", "legacy"])
-    ap.add_argument("--batches", type=int, default=CRC_BATCHES)
-    ap.add_argument("--partitions", type=int, default=1024)
+    ap.add_argument("--workload", default="finalize",
+                    choices=["finalize", "finalize_fast", "crc", "lz4c", "lz4c_fast", "lz4hc",
+                             "consumer", "producer", "serialize", "index", "legacy"])
+    ap.add_argument("--batches", type=int, default=CRC_BATCHES, help="--workload crc: batches per GPU")
+    ap.add_argument("--partitions", type=int, default=512,
+                    help="toppars (1 MiB batches) per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true")
     ap.add_argument("--level", type=int, default=9, help="compression.level of --workload lz4hc")
@@ -693,26 +943,43 @@ def main():
     if not os.path.exists(L.LIB_PATH):
         raise SystemExit(f"{L.LIB_PATH} is not built: run __graft_entry__.build()")
     L.init(device)
+    no_cpu = args.no_cpu_baseline or world > 1
 
-    if args.workload != "crc":
+    def finish():
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+
+    if args.workload not in ("finalize", "finalize_fast"):
+        # single legs (profiling, A/B runs): one short JSON line
+        if args.workload == "crc":
+            d, res = crc_leg(args, rank, world)
+            t_max = max_over_ranks(d["ms_per_step"], world)
+            if rank == 0:
+                d["GB_per_s"] = round(res["bytes"] * world / (t_max / 1e3) / 1e9, 2)
+                if not no_cpu:
+                    d["cpu_baseline"] = cpu_baseline_crc(*res["host_sample"])
+                print(json.dumps({"workload": "crc", "n_gpus": world, "steps": args.steps,
+                                  "source_hash": source_hash(), **d}), flush=True)
+            return finish()
         if args.workload == "lz4hc":
-            res = bench_lz4c(args, rank, world, level=args.level)
+            res = bench_lz4c(args, rank, world, n=args.partitions, level=args.level)
         elif args.workload.startswith("lz4c"):
-            res = bench_lz4c(args, rank, world, fast=args.workload == "lz4c_fast")
+            res = bench_lz4c(args, rank, world, n=args.partitions, fast=args.workload == "lz4c_fast")
         elif args.workload == "producer":
-            res = bench_producer(args, rank, world)
+            res = bench_producer(args, rank, world, n=args.partitions)
         elif args.workload == "serialize":
-            res = bench_serialize(args, rank, world)
+            res = bench_serialize(args, rank, world, n=args.partitions)
         elif args.workload == "index":
-            res = bench_index(args, rank, world)
+            res = bench_index(args, rank, world, n=args.partitions)
         elif args.workload == "legacy":
-            res = bench_legacy(args, rank, world)
+            res = bench_legacy(args, rank, world, n=args.partitions)
         else:
-            res = bench_consumer(args, rank, world)
+            res = bench_consumer(args, rank, world, n=args.partitions)
         t_max = max_over_ranks(res["ms"], world)
         if rank == 0:
             cpu = None
-            if not args.no_cpu_baseline and world == 1:
+            if not no_cpu:
                 if args.workload == "serialize":
                     cpu = cpu_baseline_serialize(*res["host_sample"])
                 elif args.workload == "index":
@@ -720,26 +987,31 @@ def main():
                 elif args.workload == "legacy":
                     cpu = cpu_baseline_legacy(*res["host_sample"])
                 else:
-                    cpu = cpu_baseline_lz4("decompress" if args.workload == "consumer"
-                                           else "compress",
-                                           level=args.level if args.workload == "lz4hc" else 0)
+                    cpu = cpu_reference_lz4("decompress" if args.workload == "consumer"
+                                            else "compress",
+                                            level=args.level if args.workload == "lz4hc" else 0,
+                                            with_crc=args.workload == "consumer")
             res.pop("host_sample", None)
             res["ms"] = t_max
             print(json.dumps({"workload": args.workload, "n_gpus": world, "steps": args.steps,
-                              **leg_line(args.workload, res, args.steps, world, cpu)}), flush=True)
-        if world > 1:
-            import torch.distributed as dist
-            dist.destroy_process_group()
-        return
+                              "source_hash": source_hash(),
+                              **leg_line(LEG_NAMES.get(args.workload, args.workload), res,
+                                         args.steps, world, cpu)}), flush=True)
+        return finish()
 
-    res = bench_crc(args, rank, world)
-    # whole-job time per step: max over ranks of the host clock around the
-    # K synchronised steps; the HIP-event kernel time feeds the roofline
-    t_max = max_over_ranks(res["wall_s"] * 1e3 / args.steps, world)
-    total_bytes = res["bytes"] * world
-    value = total_bytes / (t_max / 1e3) / 1e9
+    # ------------------------------------------------------------ headline
+    mode = 1 if args.workload == "finalize_fast" else 0
+    res = bench_finalize(args, rank, world, mode=mode)
+    # whole-job time per step: max over ranks of the host clock around the K synchronised
+    # steps; the HIP-event time of the compress stage feeds the roofline
+    t_max = max_over_ranks(res["ms"], world)
     if rank == 0:
-        achieved = res["alg_bytes"] / (res["kernel_ms"] / 1e3) / 1e9
+        n = res["records"]
+        value = res["bytes"] * world / (t_max / 1e3) / 1e9
+        achieved = res["comp_alg_bytes"] / (res["comp_kernel_ms"] / 1e3) / 1e9
+        leg = "writer_finalize_fast_1MiB_json" if mode else "writer_finalize_1MiB_json"
+        traffic, note = profile_summary(leg, res["comp_alg_bytes"], res["comp_kernel_ms"])
+        step_ach = res["alg_bytes"] / (res["kernel_ms"] / 1e3) / 1e9
         line = {
             "metric": "record-batch GB/s (CRC32C+LZ4F) at 1/2/4/8 GPUs; % of HBM roofline",
             "value": round(value, 2),
@@ -752,55 +1024,88 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (splitmix64 record bytes, valid v2 headers, device-generated)",
-            "config": {"workload": "configs[1]: CRC32C of 1M MsgVersion 2 record batches x 16 KiB "
-                                   "per GPU (writer finalize: CRC over [21,12+Length), stored BE at 17)",
-                       "batches_per_gpu": args.batches, "batch_bytes": CRC_BATCH_BYTES,
+            "data": "synthetic (seeded JSON-like records, valid v2 headers, device-resident)",
+            "config": {"workload": "combined CRC32C+LZ4F, writer side: rdk_hip_msgset_v2_finalize = "
+                                   "LZ4F compress (" + ("throughput compressor, reference-decodable"
+                                                        if mode else
+                                                        "frames byte-identical to rd_kafka_lz4_compress")
+                                   + ") + v2 header finalize + CRC32C finalize of 1 MiB JSON "
+                                   "MessageSets (configs[2] input, configs[4] shape), device-resident; "
+                                   "value counts uncompressed record bytes",
+                       "batches_per_gpu": n, "batch_bytes": JSON_BATCH,
                        "parallelism": f"toppar-sharded x{world}, no collective"},
-            "msgs_per_s": round(args.batches * world / (t_max / 1e3), 1),
+            "msgs_per_s": round(n * world * 9500 / (t_max / 1e3), 1),
+            "compression_ratio": round(res["ratio"], 3),
+            "source_hash": source_hash(),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": CRC_KERNEL,
-                         "alg_bytes_per_launch": res["alg_bytes"]},
+                         "traffic": traffic,
+                         "kernel": ("lz4_fast_blocks_kernel" if mode else
+                                    "lz4_compress_blocks_kernel<windows>") + " + lz4f_assemble_kernel",
+                         "kernel_ms": round(res["comp_kernel_ms"], 4),
+                         "alg_bytes_per_launch": int(res["comp_alg_bytes"]), **note,
+                         "whole_step": {"kernel_ms": round(res["kernel_ms"], 4),
+                                        "alg_bytes": int(res["alg_bytes"]),
+                                        "achieved": round(step_ach, 1),
+                                        "frac": round(step_ach / HBM_PEAK_GBS, 4)}},
             "cpu_baseline": None,
         }
-        traffic, src = pmc_traffic(CRC_PMC_SUMMARY, res["alg_bytes"])
-        if traffic is not None:
-            line["roofline"]["traffic"] = traffic
-            line["roofline"]["traffic_source"] = src
-        if not args.no_cpu_baseline and world == 1:
-            buf, n, size = res["host_sample"]
-            line["cpu_baseline"] = cpu_baseline_crc(buf, n, size)
+        if not no_cpu:
+            line["cpu_baseline"] = cpu_reference_lz4("compress", seconds=10.0, with_crc=True)
         del res
-        line["pcie_pinned"] = pcie_rates()
+        torch.cuda.empty_cache()
+        if world == 1:
+            line["pcie_pinned"] = pcie_rates()
         if not args.no_legs and world == 1:
-            # the LZ4F legs of the same path (configs[2], configs[3]) at 256 x 1 MiB
             sub = argparse.Namespace(steps=3, warmup=1, partitions=256)
-            cpu = (lambda k: None) if args.no_cpu_baseline else cpu_baseline_lz4
-            line["legs"] = {
-                "lz4f_compress_1MiB_json": leg_line("lz4c", bench_lz4c(sub, rank, world), 3, 1,
-                                                    cpu("compress")),
-                "lz4f_compress_fast_1MiB_json": leg_line(
-                    "lz4c_fast", bench_lz4c(sub, rank, world, fast=True), 3, 1, cpu("compress")),
-                # LZ4HC at its default level (LZ4HC_CLEVEL_DEFAULT = 9), 256 x 1 MiB
-                "lz4hc_compress_level9_1MiB_json": leg_line(
-                    "lz4hc", bench_lz4c(argparse.Namespace(steps=3, warmup=1, partitions=256),
-                                        rank, world, level=9), 3, 1,
-                    None if args.no_cpu_baseline else cpu_baseline_lz4("compress", level=9)),
-                "consumer_crc_verify_lz4f_decompress_1MiB": leg_line(
-                    "consumer", bench_consumer(argparse.Namespace(steps=3, warmup=1, partitions=1024),
-                                               rank, world), 3, 1, cpu("decompress")),
-                "v2_record_serialize_1MiB_json": serialize_leg(rank, world, args.no_cpu_baseline),
-                "v2_record_index_1MiB_json": index_leg(rank, world, args.no_cpu_baseline),
-                "v1_msgset_crc32_verify_1MiB_json": legacy_leg(rank, world, args.no_cpu_baseline),
-                "producer_pipeline_1MiB_json_pcie": leg_line(
-                    "producer", bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512),
-                                               rank, world), 2, 1, cpu("compress")),
-            }
+            cpu = (lambda *a, **k: None) if no_cpu else cpu_reference_lz4
+            legs = {}
+            crc_args = argparse.Namespace(steps=10, warmup=2, batches=CRC_BATCHES)
+            d, cres = crc_leg(crc_args, rank, world)
+            if not no_cpu:
+                d["cpu_baseline"] = cpu_baseline_crc(*cres["host_sample"])
+            del cres
+            torch.cuda.empty_cache()
+            legs["crc32c_only_16KiB_batches"] = d
+            other = bench_finalize(sub, rank, world, n=256, mode=1 - mode)
+            legs["writer_finalize_1MiB_json" if mode else "writer_finalize_fast_1MiB_json"] = leg_line(
+                "writer_finalize_1MiB_json" if mode else "writer_finalize_fast_1MiB_json",
+                {**other, "kernel_ms": other["comp_kernel_ms"], "alg_bytes": other["comp_alg_bytes"]},
+                3, 1, cpu("compress", with_crc=True))
+            legs["lz4f_compress_1MiB_json"] = leg_line(
+                "lz4f_compress_1MiB_json", bench_lz4c(sub, rank, world, n=256), 3, 1, cpu("compress"))
+            legs["lz4f_compress_fast_1MiB_json"] = leg_line(
+                "lz4f_compress_fast_1MiB_json", bench_lz4c(sub, rank, world, n=256, fast=True), 3, 1,
+                cpu("compress"))
+            # LZ4HC at its default level (LZ4HC_CLEVEL_DEFAULT = 9)
+            legs["lz4hc_compress_level9_1MiB_json"] = leg_line(
+                "lz4hc_compress_level9_1MiB_json", bench_lz4c(sub, rank, world, n=256, level=9), 3, 1,
+                cpu("compress", level=9))
+            legs["consumer_crc_verify_lz4f_decompress_1MiB"] = leg_line(
+                "consumer_crc_verify_lz4f_decompress_1MiB",
+                bench_consumer(argparse.Namespace(steps=3, warmup=1, partitions=1024), rank, world,
+                               n=1024), 3, 1, cpu("decompress", with_crc=True))
+            legs["v2_record_serialize_1MiB_json"] = serialize_leg(rank, world, no_cpu)
+            legs["v2_record_index_1MiB_json"] = index_leg(rank, world, no_cpu)
+            legs["v1_msgset_crc32_verify_1MiB_json"] = legacy_leg(rank, world, no_cpu)
+            legs["producer_pipeline_1MiB_json_pcie"] = leg_line(
+                "producer_pipeline_1MiB_json_pcie",
+                bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512), rank, world,
+                               n=512), 2, 1, cpu("compress", with_crc=True))
+            if not no_cpu:
+                legs["dropin_per_call_us"] = bench_dropin_calls()
+            line["legs"] = legs
         print(json.dumps(line), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    finish()
+
+
+# bench leg name of a single --workload run (profiles/r02/<leg>.json)
+LEG_NAMES = {"lz4c": "lz4f_compress_1MiB_json", "lz4c_fast": "lz4f_compress_fast_1MiB_json",
+             "lz4hc": "lz4hc_compress_level9_1MiB_json",
+             "consumer": "consumer_crc_verify_lz4f_decompress_1MiB",
+             "serialize": "v2_record_serialize_1MiB_json", "index": "v2_record_index_1MiB_json",
+             "legacy": "v1_msgset_crc32_verify_1MiB_json",
+             "producer": "producer_pipeline_1MiB_json_pcie"}
 
 
 if __name__ == "__main__":

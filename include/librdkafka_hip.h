@@ -239,6 +239,23 @@ typedef struct rdk_hip_batch_s {
 #define RDK_HIP_PRODUCER_EXACT 0 /* frames byte-identical to rd_kafka_lz4_compress */
 #define RDK_HIP_PRODUCER_FAST 1  /* rdk_hip_lz4f_compress_fast frames */
 #define RDK_HIP_E_BUSY (-5)      /* every slot is in flight: poll() first */
+/* The writer's finalize (rd_kafka_msgset_writer_finalize, rdkafka_msgset_writer.c:1335:
+ * rd_kafka_msgset_writer_compress :1128-1221 -> finalize_MessageSet_v2_header :1251-1295
+ * -> calc_crc_v2 :1229-1246) for n device-resident MessageSets in one call.  Input i is
+ * the 61-byte v2 header as the writer leaves it, immediately followed by the records at
+ * d_in + d_rec_offs[i] (d_rec_lens[i] bytes; the header sits at d_rec_offs[i] - 61).
+ * The finished batch is written to d_out + d_out_offs[i] (capacity d_out_caps[i] >=
+ * 61 + rdk_hip_lz4f_compress_bound(len); offsets 16-byte aligned): header with Length
+ * and the LZ4 codec bits set, the LZ4F frame (or the plain records when the frame would
+ * be larger, :1179), CRC32C stored at offset 17.  d_frame_lens[i] = frame size,
+ * d_batch_lens[i] = 12 + Length, d_crcs[i] = the CRC.  mode is RDK_HIP_PRODUCER_EXACT
+ * (frames byte-identical to rd_kafka_lz4_compress at level 0) or _FAST.  This is what
+ * the producer front-end runs per staging slot. */
+int rdk_hip_msgset_v2_finalize(const void *d_in, const uint64_t *d_rec_offs,
+                               const uint32_t *d_rec_lens, void *d_out,
+                               const uint64_t *d_out_offs, const uint32_t *d_out_caps,
+                               uint32_t *d_frame_lens, uint32_t *d_batch_lens,
+                               uint32_t *d_crcs, uint32_t n, int mode, void *stream);
 rdk_hip_producer_t *rdk_hip_producer_new(int device, size_t slot_bytes, int nslots, int mode);
 int rdk_hip_producer_produce(rdk_hip_producer_t *p, const void *hdr61, const void *records,
                              uint32_t len, uint64_t cookie);

@@ -51,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "rdk_hip_producer_flush", "rdk_hip_producer_poll", "rdk_hip_producer_destroy",
     "rdk_hip_gen_json", "rdk_hip_msgset_v2_sizes", "rdk_hip_msgset_v2_write",
     "rdk_hip_msgset_v2_index", "rd_slice_crc32", "rdk_hip_crc32_ranges",
-    "rdk_hip_msgset_v01_crc", "rdk_hip_lz4f_decompress_noalloc",
+    "rdk_hip_msgset_v01_crc", "rdk_hip_lz4f_decompress_noalloc", "rdk_hip_msgset_v2_finalize",
 )
 
 
@@ -111,6 +111,8 @@ def lib():
         L.rdk_hip_lz4f_decompress.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
         L.rdk_hip_lz4f_decompress_noalloc.restype = i32
         L.rdk_hip_lz4f_decompress_noalloc.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
+    L.rdk_hip_msgset_v2_finalize.restype = i32
+    L.rdk_hip_msgset_v2_finalize.argtypes = [vp] * 9 + [u32, i32, vp]
     L.rdk_hip_producer_new.restype = vp
     L.rdk_hip_producer_new.argtypes = [i32, sz, i32, i32]
     L.rdk_hip_producer_produce.restype = i32
@@ -384,6 +386,16 @@ def lz4f_decompress_batch_noalloc(src, in_offs, in_lens, dst, out_offs, out_caps
 
 PRODUCER_EXACT, PRODUCER_FAST = 0, 1
 E_BUSY = -5
+
+
+def msgset_v2_finalize(src, rec_offs, rec_lens, dst, out_offs, out_caps, frame_lens, batch_lens,
+                       crcs, mode=PRODUCER_EXACT, stream=None) -> None:
+    """rdk_hip_msgset_v2_finalize: the writer's compress + header finalize + CRC32C
+    (rdkafka_msgset_writer.c:1335) for device-resident MessageSets."""
+    _check(lib().rdk_hip_msgset_v2_finalize(_ptr(src), _ptr(rec_offs), _ptr(rec_lens), _ptr(dst),
+                                            _ptr(out_offs), _ptr(out_caps), _ptr(frame_lens),
+                                            _ptr(batch_lens), _ptr(crcs), int(rec_offs.numel()),
+                                            mode, _stream(stream)), "msgset_v2_finalize")
 
 
 class _Batch(C.Structure):

@@ -27,13 +27,19 @@ struct Ctx {
   size_t h_cap = 0;
   // device scratch (grow-only), independent regions: kScratchStage is the drop-in
   // symbols' staging (only ever used on `stream`, which every drop-in call leaves
-  // idle); kScratchDecode / kScratchHc / kScratchCrc hold the batch API's descriptors, the
-  // LZ4HC tables and the split CRC's partial registers and follow the caller's streams (scratch_acquire / _release)
+  // idle); kScratchDecode / kScratchHc hold the batch API's descriptors and the
+  // LZ4HC tables and follow the caller's streams (scratch_acquire / _release)
   uint8_t *d_stage[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t d_cap[4] = {0, 0, 0, 0};
   hipStream_t d_last[4] = {nullptr, nullptr, nullptr, nullptr};  // stream of the last user
   hipEvent_t d_done[4] = {nullptr, nullptr, nullptr, nullptr};  // recorded after the last use
   bool d_used[4] = {false, false, false, false};
+  // the split CRC's partial registers (64 KiB), one buffer per caller stream: calls on
+  // different streams never meet, so no event or allocation orders them
+  static constexpr int kCrcStreams = 32;
+  hipStream_t crc_stream[kCrcStreams] = {};
+  uint32_t *crc_buf[kCrcStreams] = {};
+  int crc_streams = 0;
   // small device descriptor buffer
   uint8_t *d_desc = nullptr;
   size_t d_desc_cap = 0;
@@ -53,6 +59,8 @@ constexpr int kScratchRegions = 4;
 // region has to grow), release marks the end of this use on `s`.
 int scratch_acquire(Ctx *c, int which, size_t bytes, hipStream_t s);
 int scratch_release(Ctx *c, int which, hipStream_t s);
+// 64 KiB of device words private to (this thread, stream s); nullptr with the error set
+uint32_t *crc_scratch(Ctx *c, hipStream_t s);
 
 // Device-resident CRC tables for `device` (uploaded once per device).  kind selects the
 // polynomial: kCrcKind32C (CRC-32C, crc32c.c) or kCrcKind32 (CRC-32/zlib, rdcrc32.h).

@@ -930,17 +930,17 @@ static int launch_v2_any(Ctx *c, uint8_t *b, const uint64_t *offs, const uint32_
   constexpr uint32_t kSlots = 256u * kV4Groups;
   if (crc_variant() == 4 && n <= kSlots / 2) {
     const uint32_t nch = std::min(64u, kSlots / n);
-    // at most kSlots partial registers (64 KiB): the thread's kScratchCrc region
-    int rc = scratch_acquire(c, kScratchCrc, size_t(kSlots) * 4, s);
-    if (rc) return rc;
-    uint32_t *raw = reinterpret_cast<uint32_t *>(c->d_stage[kScratchCrc]);
+    // at most kSlots partial registers (64 KiB), private to this thread and stream
+    static_assert(size_t(kSlots) * 4 <= 65536, "crc_scratch() holds 64 KiB");
+    uint32_t *raw = crc_scratch(c, s);
+    if (!raw) return RDK_HIP_E_NOMEM;
     const uint32_t items = n * nch;
     hipLaunchKernelGGL(crc32c_msgset_v2_split_kernel, dim3(crc_grid_v4(items)), dim3(kV4Block),
                        0, s, b, offs, caps, n, nch, raw, crc_tables_v4_dev(c->device));
     hipLaunchKernelGGL(crc32c_msgset_v2_combine_kernel<MODE>, dim3((n + 63) / 64), dim3(64), 0,
                        s, b, offs, caps, n, nch, raw, out, crc_x2n_dev(c->device));
     RDK_HIP_CHECK(hipGetLastError());
-    return scratch_release(c, kScratchCrc, s);
+    return RDK_HIP_OK;
   } else if (crc_variant() == 4)
     hipLaunchKernelGGL(crc32c_msgset_v2_v4_kernel<MODE>, dim3(crc_grid_v4(n)), dim3(kV4Block), 0,
                        s, b, offs, caps, out, n, crc_tables_v4_dev(c->device));

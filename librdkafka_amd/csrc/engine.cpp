@@ -113,6 +113,8 @@ int bind(int dev) {
       if (tl_ctx->d_done[i]) (void)hipEventDestroy(tl_ctx->d_done[i]);
       tl_ctx->d_done[i] = nullptr;
     }
+    for (int i = 0; i < tl_ctx->crc_streams; ++i) (void)hipFree(tl_ctx->crc_buf[i]);
+    tl_ctx->crc_streams = 0;
     if (tl_ctx->d_desc) (void)hipFree(tl_ctx->d_desc);
     tl_ctx->d_desc = nullptr;
     tl_ctx->d_desc_cap = 0;
@@ -204,6 +206,24 @@ int scratch_release(Ctx *c, int which, hipStream_t s) {
   c->d_last[which] = s;
   c->d_used[which] = true;
   return 0;
+}
+
+uint32_t *crc_scratch(Ctx *c, hipStream_t s) {
+  for (int i = 0; i < c->crc_streams; ++i)
+    if (c->crc_stream[i] == s) return c->crc_buf[i];
+  int slot = c->crc_streams;
+  if (slot == Ctx::kCrcStreams) {
+    // more streams than slots: recycle the oldest once its stream has drained
+    slot = 0;
+    if (hipStreamSynchronize(c->crc_stream[0]) != hipSuccess) (void)hipGetLastError();
+  } else {
+    uint8_t *p = nullptr;
+    if (dev_alloc(&p, 65536)) return nullptr;
+    c->crc_buf[slot] = reinterpret_cast<uint32_t *>(p);
+    c->crc_streams++;
+  }
+  c->crc_stream[slot] = s;
+  return c->crc_buf[slot];
 }
 
 // drop-in symbols only (c->stream, idle between calls)

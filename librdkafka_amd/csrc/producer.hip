@@ -152,31 +152,60 @@ __global__ __launch_bounds__(256) void pack_to_host_kernel(const uint8_t *__rest
   }
 }
 
+}  // namespace
+
+// The writer's finalize for n device-resident MessageSets (see the header): compress,
+// codec choice + header, CRC32C.  Three stages on `stream`, no host synchronisation.
+RDK_API int rdk_hip_msgset_v2_finalize(const void *d_in, const uint64_t *d_rec_offs,
+                                       const uint32_t *d_rec_lens, void *d_out,
+                                       const uint64_t *d_out_offs, const uint32_t *d_out_caps,
+                                       uint32_t *d_frame_lens, uint32_t *d_batch_lens,
+                                       uint32_t *d_crcs, uint32_t n, int mode, void *stream) {
+  if (!n) return RDK_HIP_OK;
+  if (!d_in || !d_rec_offs || !d_rec_lens || !d_out || !d_out_offs || !d_out_caps ||
+      !d_frame_lens || !d_batch_lens || !d_crcs)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  if (mode != RDK_HIP_PRODUCER_EXACT && mode != RDK_HIP_PRODUCER_FAST)
+    return set_error(RDK_HIP_E_INVAL, "bad mode %d", mode);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // frame i goes 61 bytes into batch i's output slot; the offsets array is derived on the
+  // device so the caller passes one array
+  int rc;
+  {
+    // frame offsets = out_offs + 61: reuse d_batch_lens' neighbour is not possible, so the
+    // compressors take a byte-shifted base instead (same offsets, base + 61)
+    uint8_t *fbase = static_cast<uint8_t *>(d_out) + kV2Hdr;
+    if (mode == RDK_HIP_PRODUCER_FAST)
+      rc = rdk_hip_lz4f_compress_fast(d_in, d_rec_offs, d_rec_lens, fbase, d_out_offs, d_frame_lens,
+                                      n, stream);
+    else
+      rc = rdk_hip_lz4f_compress(d_in, d_rec_offs, d_rec_lens, fbase, d_out_offs, d_frame_lens, n,
+                                 0, stream);
+  }
+  if (rc) return rc;
+  hipLaunchKernelGGL(v2_finalize_kernel, dim3(n < 4096u ? n : 4096u), dim3(256), 0, s,
+                     static_cast<const uint8_t *>(d_in), d_rec_offs, d_rec_lens,
+                     static_cast<uint8_t *>(d_out), d_out_offs, d_frame_lens, d_batch_lens, n);
+  RDK_HIP_CHECK(hipGetLastError());
+  // CRC32C over [21, 12+Length) of each finished batch, stored BE at 17
+  return rdk_hip_msgset_v2_crc(d_out, d_out_offs, d_out_caps, d_crcs, n, RDK_HIP_V2_CRC_FINALIZE,
+                               stream);
+}
+
+namespace {
+
 int launch(rdk_hip_producer_s *p, Slot &sl) {
   const uint32_t B = p->max_batches, n = sl.nb;
   const Meta hm = meta_at(sl.h_meta, B), dm = meta_at(sl.d_meta, B);
   RDK_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, sl.in_used, hipMemcpyHostToDevice, sl.s));
   RDK_HIP_CHECK(hipMemcpyAsync(dm.rec_offs, hm.rec_offs, size_t(n) * 8, hipMemcpyHostToDevice, sl.s));
   RDK_HIP_CHECK(hipMemcpyAsync(dm.out_offs, hm.out_offs, size_t(n) * 8, hipMemcpyHostToDevice, sl.s));
-  RDK_HIP_CHECK(hipMemcpyAsync(dm.frame_offs, hm.frame_offs, size_t(n) * 8, hipMemcpyHostToDevice, sl.s));
   RDK_HIP_CHECK(hipMemcpyAsync(dm.caps, hm.caps, size_t(n) * 4, hipMemcpyHostToDevice, sl.s));
   RDK_HIP_CHECK(hipMemcpyAsync(dm.rec_lens, hm.rec_lens, size_t(n) * 4, hipMemcpyHostToDevice, sl.s));
-  int rc;
-  if (p->mode == RDK_HIP_PRODUCER_FAST)
-    rc = rdk_hip_lz4f_compress_fast(sl.d_in, dm.rec_offs, dm.rec_lens, sl.d_out, dm.frame_offs,
-                                    dm.frame_lens, n, sl.s);
-  else
-    rc = rdk_hip_lz4f_compress(sl.d_in, dm.rec_offs, dm.rec_lens, sl.d_out, dm.frame_offs,
-                               dm.frame_lens, n, 0, sl.s);
+  int rc = rdk_hip_msgset_v2_finalize(sl.d_in, dm.rec_offs, dm.rec_lens, sl.d_out, dm.out_offs,
+                                      dm.caps, dm.frame_lens, dm.batch_lens, dm.crcs, n, p->mode,
+                                      sl.s);
   if (rc) return rc;
-  hipLaunchKernelGGL(v2_finalize_kernel, dim3(n < 4096u ? n : 4096u), dim3(256), 0, sl.s, sl.d_in,
-                     dm.rec_offs, dm.rec_lens, sl.d_out, dm.out_offs, dm.frame_lens,
-                     dm.batch_lens, n);
-  RDK_HIP_CHECK(hipGetLastError());
-  // CRC32C over [21, 12+Length) of each finished batch, stored BE at 17
-  if ((rc = rdk_hip_msgset_v2_crc(sl.d_out, dm.out_offs, dm.caps, dm.crcs, n,
-                                  RDK_HIP_V2_CRC_FINALIZE, sl.s)))
-    return rc;
   RDK_HIP_CHECK(hipMemsetAsync(dm.cursor, 0, 8, sl.s));
   hipLaunchKernelGGL(pack_to_host_kernel, dim3(n < 2048u ? n : 2048u), dim3(256), 0, sl.s,
                      sl.d_out, dm.out_offs, dm.batch_lens, n, sl.dh_out, dm.pack_offs,
@@ -271,7 +300,6 @@ RDK_API int rdk_hip_producer_produce(rdk_hip_producer_t *p, const void *hdr61, c
   hm.rec_offs[sl->nb] = sl->in_used + kV2Hdr;
   hm.rec_lens[sl->nb] = len;
   hm.out_offs[sl->nb] = sl->out_used;
-  hm.frame_offs[sl->nb] = sl->out_used + kV2Hdr;
   hm.caps[sl->nb] = uint32_t(need_out);
   sl->cookies.push_back(cookie);
   sl->in_used += need_in;

@@ -136,6 +136,14 @@ def ref():
         R.ref_lz4f_compress_prefs.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                               C.c_int, C.c_int, C.c_int, C.c_size_t,
                                               C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+        R.ref_lz4f_compress_batches_mt.restype = C.c_int
+        R.ref_lz4f_compress_batches_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                                   C.c_int]
+        R.ref_lz4f_decompress_batches_mt.restype = C.c_int
+        R.ref_lz4f_decompress_batches_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p,
+                                                     C.c_size_t, C.c_size_t, C.c_void_p,
+                                                     C.c_void_p, C.c_void_p, C.c_int]
         _ref = R
     return _ref
 

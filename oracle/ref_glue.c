@@ -218,3 +218,86 @@ done:
     if (err) free(out);
     return err;
 }
+
+/* ---- timed CPU baseline: many batches on `threads` host threads, each batch through
+ * the drivers above, i.e. through the reference's own compiled lz4frame.c / lz4.c /
+ * lz4hc.c with rd_kafka_lz4_compress's / _decompress's allocation pattern (malloc of
+ * LZ4F_compressBound+1000 and a fresh LZ4F context per call, rdkafka_lz4.c:351-376;
+ * inlen*4 estimate and x1.75 regrowth, :218-286).  out_lens[i] = frame / payload size;
+ * the bytes are copied to out + out_offs[i] when out is not NULL. */
+#include <pthread.h>
+
+struct ref_job {
+    int decompress, level, threads, tid;
+    const char *base;
+    const uint64_t *offs;
+    const uint32_t *lens;
+    size_t n, max_msg_size;
+    char *out;
+    const uint64_t *out_offs;
+    uint32_t *out_lens;
+    int err;
+};
+
+static void *ref_worker(void *arg) {
+    struct ref_job *j = arg;
+    for (size_t i = (size_t)j->tid; i < j->n; i += (size_t)j->threads) {
+        char *o = NULL;
+        size_t olen = 0;
+        int e;
+        if (j->decompress) {
+            int grow;
+            /* the reader hands rd_kafka_lz4_decompress a contiguous, writable slice */
+            e = ref_rdk_lz4_decompress(1, (char *)j->base + j->offs[i], j->lens[i],
+                                       j->max_msg_size, &o, &olen, &grow);
+        } else {
+            const char *seg = j->base + j->offs[i];
+            size_t sl = j->lens[i];
+            e = ref_rdk_lz4_compress(1, j->level, &seg, &sl, 1, &o, &olen);
+        }
+        if (e) { j->err = e; continue; }
+        j->out_lens[i] = (uint32_t)olen;
+        if (j->out) memcpy(j->out + j->out_offs[i], o, olen);
+        free(o);
+    }
+    return NULL;
+}
+
+static int ref_run_mt(struct ref_job proto, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    struct ref_job jobs[256];
+    int err = 0;
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = proto;
+        jobs[t].threads = threads;
+        jobs[t].tid = t;
+        jobs[t].err = 0;
+        pthread_create(&th[t], NULL, ref_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].err) err = jobs[t].err;
+    }
+    return err;
+}
+
+int ref_lz4f_compress_batches_mt(const char *base, const uint64_t *offs, const uint32_t *lens,
+                                 size_t n, char *out, const uint64_t *out_offs,
+                                 uint32_t *out_lens, int level, int threads) {
+    struct ref_job p = {0};
+    p.level = level; p.base = base; p.offs = offs; p.lens = lens; p.n = n;
+    p.out = out; p.out_offs = out_offs; p.out_lens = out_lens;
+    return ref_run_mt(p, threads);
+}
+
+int ref_lz4f_decompress_batches_mt(const char *base, const uint64_t *offs, const uint32_t *lens,
+                                   size_t n, size_t max_msg_size, char *out,
+                                   const uint64_t *out_offs, uint32_t *out_lens, int threads) {
+    struct ref_job p = {0};
+    p.decompress = 1; p.base = base; p.offs = offs; p.lens = lens; p.n = n;
+    p.max_msg_size = max_msg_size;
+    p.out = out; p.out_offs = out_offs; p.out_lens = out_lens;
+    return ref_run_mt(p, threads);
+}

@@ -84,3 +84,45 @@ def test_producer_order_and_busy(engine):
     p.flush()
     assert [c for c, _, _ in p.poll(block=True)] == [2]
     p.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_msgset_v2_finalize_device_batches(engine, oracle_mod, mode):
+    """rdk_hip_msgset_v2_finalize on device-resident MessageSets (the writer's compress +
+    header finalize + CRC32C in one call): every finished batch checked field by field
+    against the oracle, the frame byte for byte in exact mode."""
+    import numpy as np
+    import torch
+    rnd = random.Random(60 + mode)
+    sizes = [0, 1, 13, 4096, 65536, 65537, 300000, 1 << 20] + \
+            [rnd.randrange(1, 150000) for _ in range(30)]
+    items = []
+    for i, n in enumerate(sizes):
+        rec = W.gen_json(n, 100 + i) if i % 4 else rnd.randbytes(n)
+        hdr = bytearray(W.v2_header(i, 61 + n))
+        hdr[21:23] = (0x10 if i % 3 == 0 else 0).to_bytes(2, "big")
+        items.append((bytes(hdr), rec))
+    in_offs, pos = [], 0
+    for hdr, rec in items:
+        in_offs.append(pos + 61)
+        pos += (61 + len(rec) + 63) // 64 * 64
+    hbuf = bytearray(pos + 256)
+    for o, (hdr, rec) in zip(in_offs, items):
+        hbuf[o - 61:o] = hdr
+        hbuf[o:o + len(rec)] = rec
+    caps = [(61 + engine.lz4f_compress_bound(len(rec)) + 255) // 256 * 256 for _, rec in items]
+    out_offs = np.concatenate([[0], np.cumsum(caps)[:-1]])
+    n = len(items)
+    d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
+    d_out = torch.zeros(int(sum(caps)) + 256, dtype=torch.uint8, device="cuda")
+    t64 = lambda a: torch.tensor(np.asarray(a, dtype=np.int64), device="cuda")  # noqa: E731
+    t32 = lambda a: torch.tensor(np.asarray(a, dtype=np.int32), device="cuda")  # noqa: E731
+    flens, blens, crcs = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    engine.msgset_v2_finalize(d_in, t64(in_offs), t32([len(r) for _, r in items]), d_out,
+                              t64(out_offs), t32(caps), flens, blens, crcs, mode=mode)
+    host = bytes(d_out.cpu().numpy())
+    bl = blens.cpu().numpy()
+    cr = crcs.cpu().numpy().view(np.uint32)
+    for i, (hdr, rec) in enumerate(items):
+        out = host[out_offs[i]:out_offs[i] + bl[i]]
+        _check_batch(oracle_mod, hdr, rec, out, int(cr[i]), mode == 0)

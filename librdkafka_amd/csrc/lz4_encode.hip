@@ -315,6 +315,7 @@ __device__ __forceinline__ bool generic_search(uintptr_t src, int mflimitPlusOne
 }
 
 constexpr int kRegLen = 28;   // match bytes a lane measures from its two register windows
+constexpr int kMaxLen = 92;   // ... and with up to 64 more bytes from the source ring
 constexpr int kRegBack = 4;   // catch-up bytes a lane measures from them
 constexpr uint32_t kShortLit = 16;  // literal runs copied by their own lane
 
@@ -412,8 +413,9 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   // ---------------------------------------------------------------- per lane
   const int i = w0 + lane;
   const bool act = i <= b.n - kLz4MFLimit;  // position + 1 <= mflimitPlusOne
-  // the ring covers this window's own bytes: positions w0 .. w0+63 and 35 bytes beyond
-  while (b.H < w0 + int(b.sa) + 64 + 36) ring_fill(b, lane);
+  // the ring covers this window's own bytes (positions w0 .. w0+63 and 35 bytes beyond) and
+  // the bytes a lane compares when it measures a match past its register window
+  while (b.H < w0 + int(b.sa) + 64 + kMaxLen + 8) ring_fill(b, lane);
   uint32_t xd[9], yt[9];
   ring_load9(b, (uint32_t(i) + b.sa) & ~3u, xd);
   const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
@@ -452,7 +454,31 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
                        __builtin_amdgcn_alignbyte(yt[k + 2], yt[k + 1], shc);
     if (z) len = 4 * k + (__builtin_ctz(z) >> 3);
   }
+  // a match that fills the register window is measured on from the ring, 4 bytes a step, up
+  // to kMaxLen; `sat` = the length is still not final (kMaxLen reached, or a candidate older
+  // than the ring) and has to be finished from memory if the parse takes this match
+  bool more = tver && len == kRegLen && !far;
+  if (ballot(more)) {
+    const uint32_t vi = uint32_t(i) + b.sa, vc = uint32_t(tc) + b.sa;
+#pragma unroll 1
+    for (int j = 0; j < (kMaxLen - kRegLen) / 4; ++j) {
+      if (!ballot(more)) break;
+      const uint32_t pi = vi + uint32_t(len), pc = vc + uint32_t(len);
+      lds_u8 *rb = (lds_u8 *)b.ring;
+      const uint32_t a0 = *(lds_u32 *)(rb + (pi & (kRingBytes - 4u)));
+      const uint32_t a1 = *(lds_u32 *)(rb + ((pi + 4u) & (kRingBytes - 4u)));
+      const uint32_t c0 = *(lds_u32 *)(rb + (pc & (kRingBytes - 4u)));
+      const uint32_t c1 = *(lds_u32 *)(rb + ((pc + 4u) & (kRingBytes - 4u)));
+      const uint32_t z = __builtin_amdgcn_alignbyte(a1, a0, pi & 3u) ^
+                         __builtin_amdgcn_alignbyte(c1, c0, pc & 3u);
+      if (more) {
+        len += z ? int(__builtin_ctz(z) >> 3) : 4;
+        if (z) more = false;
+      }
+    }
+  }
   if (len > b.mlim - i) len = b.mlim - i;  // LZ4_count stops at matchlimit
+  const bool sat = tver && i + len < b.mlim && (len == kMaxLen || (far && len == kRegLen));
   const uint32_t back = __builtin_amdgcn_alignbyte(xd[1], xd[0], shi);  // bytes i-4 .. i-1
   const uint32_t xb = back ^ __builtin_amdgcn_alignbyte(yt[1], yt[0], shc);
   int bkr = xb ? int(__builtin_clz(xb) >> 3) : kRegBack;
@@ -460,7 +486,8 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   const int NA = ~ACT ? __builtin_ctzll(~ACT) : 64;  // first lane that may not be probed
 
   // one readlane per sequence fetches the lane's candidate, match length and catch-up
-  const uint32_t pk = uint32_t(tc) | (uint32_t(len) << 16) | (uint32_t(bkr) << 24);
+  const uint32_t pk = uint32_t(tc) | (uint32_t(len) << 16) | (uint32_t(bkr) << 24) |
+                      (sat ? 1u << 27 : 0u);
   const uint64_t VD = VT | DUP;  // lanes >= NA have neither bit
 
   // ------------------------------------------------------------- scalar walk
@@ -496,6 +523,97 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
     }                                                                                       \
   } while (0)
 
+  // ------------------------------------------------------------ parallel walk
+  // Matches hop from one verified lane to the next: f(m) = first verified lane at or after
+  // m + len[m]; the chosen lanes are the orbit of f from the entry, found by pointer
+  // doubling (a match is at least 4 long, so at most 16 fit in a window).  This assumes
+  // every candidate is the table's (no lane of this window supplies one); that and the rare
+  // shapes (length or catch-up not final, strides above 1, end of block) are checked
+  // afterwards, and the scalar walk below redoes the window when a check fails.
+  bool fast_done = false;
+  if (NA == 64 && mode != W_FORCED) {
+    const int e = mode == W_POSTMATCH ? 2 : 0;
+    const int tl = lane + len;
+    const uint64_t fm = tl >= 64 ? 0ull : VT & (~0ull << tl);
+    const int J0 = fm ? __builtin_ctzll(fm) : 64;
+    // (every lane takes part in each shuffle: a lane that is switched off reads as 0)
+    const int s1 = __shfl(J0, J0 & 63);
+    const int J1 = J0 < 64 ? s1 : 64;
+    const int s2 = __shfl(J1, J1 & 63);
+    const int J2 = J1 < 64 ? s2 : 64;
+    const int s3 = __shfl(J2, J2 & 63);
+    const int J3 = J2 < 64 ? s3 : 64;
+    const uint64_t em = VT & ~bits_below(e);
+    int pos = em ? __builtin_ctzll(em) : 64;  // lane k < 16 looks up the k-th match
+    {
+      const int p0 = __shfl(J0, pos & 63);
+      if ((lane & 1) && pos < 64) pos = p0;
+      const int p1 = __shfl(J1, pos & 63);
+      if ((lane & 2) && pos < 64) pos = p1;
+      const int p2 = __shfl(J2, pos & 63);
+      if ((lane & 4) && pos < 64) pos = p2;
+      const int p3 = __shfl(J3, pos & 63);
+      if ((lane & 8) && pos < 64) pos = p3;
+    }
+    // OR of (1 << pos) over lanes 0..15: a DPP scan inside the first row
+    uint32_t blo = (lane < 16 && pos < 32) ? 1u << pos : 0u;
+    uint32_t bhi = (lane < 16 && pos >= 32 && pos < 64) ? 1u << (pos - 32) : 0u;
+#define RDK_ROW_OR(v)                                                                  \
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, true));      \
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, true));      \
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, true));      \
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, true));
+    RDK_ROW_OR(blo)
+    RDK_ROW_OR(bhi)
+#undef RDK_ROW_OR
+    const uint64_t ch = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(bhi), 15))) << 32) |
+                        uint32_t(__builtin_amdgcn_readlane(int(blo), 15));
+    // per lane: the end of the previous chosen match
+    const uint64_t lowc = ch & ((1ull << lane) - 1ull);
+    const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
+    const int pend = __shfl(i + len, pl);
+    const bool isch = (ch >> lane) & 1ull;
+    const bool interior = lowc && pend > i;
+    const uint64_t Mv = ballot(lane >= e && !interior);
+    uint64_t Tm = ballot(lowc && pend == i);
+    uint64_t Rm = ballot(lowc && pend == i + 2 && pend - w0 < 64);
+    if (mode == W_POSTMATCH) {
+      Tm |= 4ull;
+      Rm |= 1ull;
+    }
+    const uint64_t ins = Mv | Rm;
+    const int prev = lowc ? pend : anchor_in;
+    const int blim = i - prev < tc ? i - prev : tc;  // lz4.c:958: ip>anchor, match>lowLimit
+    const int fbk = bkr < blim ? bkr : blim;
+    const bool bad = (isch && ((bkr == kRegBack && blim > kRegBack) || sat || i + len >= b.mfl1)) ||
+                     (((Mv >> lane) & 1ull) && (eq & ins & ((1ull << lane) - 1ull)));
+    const int x1 = ch ? __builtin_ctzll(ch) : 63;
+    if (!ballot(bad) && !(mode == W_SEARCH && b.cnt + x1 > 64)) {
+      fast_done = true;
+      INS = ins;
+      chosen = ch;
+      L_cand = tc;
+      L_len = len;
+      L_bk = fbk;
+      if (ch) {
+        const int cl = 63 - __builtin_clzll(ch);
+        const int end = cl + __builtin_amdgcn_readlane(len, cl);  // lane after the last match
+        anchor = w0 + end;
+        if (end >= 64) {
+          b.ip = w0 + end;
+          b.mode = W_POSTMATCH;
+        } else {
+          b.ip = w0 + 64;
+          b.cnt = 63 - (63 - __builtin_clzll(Tm));  // probes after the last re-tested lane
+        }
+      } else {
+        b.ip = w0 + 64;
+        b.cnt = Tm ? 63 - (63 - __builtin_clzll(Tm)) : b.cnt + 64;
+      }
+    }
+  }
+
+  if (!fast_done) {
   bool have = false;  // a verified match at lane x is pending
   bool post = false;  // a match just ended at ipn
   if (mode == W_POSTMATCH) {
@@ -517,10 +635,10 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
         fl = win_count_fwd(b, P + 4, cand + 4, b.mlim - (P + 4), lane);
         bk = wave_count_back(b.src + uint32_t(P), b.src + uint32_t(cand), blim, lane);
       } else {
-        const int lx = int((pkx >> 16) & 0xFFu), bx = int(pkx >> 24);
+        const int lx = int((pkx >> 16) & 0xFFu), bx = int((pkx >> 24) & 7u);
         fl = lx - 4;
-        if (lx == kRegLen && P + kRegLen < b.mlim)
-          fl += win_count_fwd(b, P + kRegLen, cand + kRegLen, b.mlim - P - kRegLen, lane);
+        if (pkx & (1u << 27))  // length not final: finish it from the ring / memory
+          fl += win_count_fwd(b, P + lx, cand + lx, b.mlim - P - lx, lane);
         bk = bx < blim ? bx : blim;
         if (bx == kRegBack && blim > kRegBack)
           bk = kRegBack + wave_count_back(b.src + uint32_t(P - kRegBack),
@@ -595,6 +713,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
       have = true;
     }
   }
+  }  // !fast_done
 #undef RDK_WIN_LOOKUP
 
   // ------------------------------------------------------------ table update
@@ -750,7 +869,11 @@ __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
   const int lane = threadIdx.x;
   const uint64_t items = uint64_t(n) * kEncMaxItems;
   for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
-    const uint32_t f = uint32_t(it / kEncMaxItems), kk = uint32_t(it % kEncMaxItems);
+    // slot-major items: all frames' block 0, then all block 1, ...  The blocks that exist
+    // come first and are dense in blockIdx, so they spread over every XCD, shader engine
+    // and CU (a frame-major order parks the missing blocks of short frames in a periodic
+    // pattern that leaves half of the shader engines idle)
+    const uint32_t f = uint32_t(it % n), kk = uint32_t(it / n);
     const uint32_t len = uni(in_lens[f]);
     const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
     for (uint32_t k = kk; k < nb; k += kEncMaxItems) {
@@ -883,6 +1006,7 @@ int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const 
 }  // namespace rdk
 
 using namespace rdk;
+
 
 RDK_API size_t rdk_hip_lz4f_compress_bound(size_t len) { return lz4f_compress_bound(len); }
 

@@ -289,7 +289,11 @@ __global__ __launch_bounds__(64) void lz4_fast_blocks_kernel(
   const int lane = threadIdx.x;
   const uint64_t items = uint64_t(n) * kFastMaxItems;
   for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
-    const uint32_t f = uint32_t(it / kFastMaxItems), kk = uint32_t(it % kFastMaxItems);
+    // slot-major items: all frames' block 0, then all block 1, ...  The blocks that exist
+    // come first and are dense in blockIdx, so they spread over every XCD, shader engine
+    // and CU (a frame-major order parks the missing blocks of short frames in a periodic
+    // pattern that leaves half of the shader engines idle)
+    const uint32_t f = uint32_t(it % n), kk = uint32_t(it / n);
     const uint32_t len = uni(in_lens[f]);
     const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
     for (uint32_t k = kk; k < nb; k += kFastMaxItems) {

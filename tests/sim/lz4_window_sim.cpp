@@ -18,7 +18,8 @@
 namespace {
 
 constexpr int kMinMatch = 4, kLastLiterals = 5, kMFLimit = 12;
-constexpr int kRegLen = 28;   // match bytes a lane measures from its register windows
+constexpr int kRegLen = 92;   // match bytes a lane measures itself (28 from its register
+                              // windows, up to 64 more from the source ring)
 constexpr int kRegBack = 4;   // catch-up bytes a lane measures from its register windows
 
 struct Block {
@@ -28,7 +29,7 @@ struct Block {
   uint16_t table[1 << 13];
   int ip, cnt, anchor, op;
   // statistics for the test: how often each path ran
-  long windows, generic, inwin, longfwd, longback;
+  long windows, generic, inwin, longfwd, longback, fastwin;
 };
 
 inline uint32_t rd32(const uint8_t *p) {
@@ -144,6 +145,87 @@ Status window(Block &b, int w0, Mode mode, int forced_cand, Mode &next_mode) {
     return (VT >> lx) & 1;
   };
 
+  // ---- parallel walk (the kernel's fast path).  Matches hop from one verified lane to the
+  // next: f(m) = first verified lane at or after m + len[m]; the chosen lanes are the orbit
+  // of f from the entry, found by pointer doubling (at most 16 matches fit in a window).
+  // It assumes every candidate is the table's (no lane of this window supplies one); that
+  // and the rare shapes are checked afterwards, and the scalar walk below redoes the window
+  // when a check fails.
+  bool fast_done = false;
+  if (NA == 64 && mode != FORCED) {
+    auto first_vt = [&](int from) { return from >= 64 ? 64 : ((VT & ~below(from)) ? __builtin_ctzll(VT & ~below(from)) : 64); };
+    const int e = mode == POSTMATCH ? 2 : 0;
+    int J[64];
+    for (int l = 0; l < 64; ++l) J[l] = first_vt(l + len[l]);       // meaningful on VT lanes
+    int Jd[4][65];
+    for (int l = 0; l < 64; ++l) Jd[0][l] = J[l];
+    Jd[0][64] = 64;
+    for (int d = 1; d < 4; ++d) {
+      for (int l = 0; l < 64; ++l) Jd[d][l] = Jd[d - 1][Jd[d - 1][l]];
+      Jd[d][64] = 64;
+    }
+    uint64_t ch = 0;
+    for (int k = 0; k < 16; ++k) {                                    // lane k: k-th match
+      int pos = first_vt(e);
+      for (int d = 0; d < 4; ++d)
+        if ((k >> d) & 1) pos = Jd[d][pos];
+      if (pos < 64) ch |= 1ull << pos;
+    }
+    // per lane: the previous chosen lane's end
+    bool ok = true;
+    uint64_t Mv = 0, Tm = 0, Rm = 0;
+    int f_cand[64], f_len[64], f_bk[64];
+    for (int l = 0; l < 64; ++l) {
+      const int i = w0 + l;
+      const uint64_t lowc = ch & below(l);
+      const int pl = lowc ? 63 - __builtin_clzll(lowc) : -1;
+      const int pend = pl >= 0 ? w0 + pl + len[pl] : 0;
+      const bool interior = pl >= 0 && pend > i;
+      if (l >= e && !interior) Mv |= 1ull << l;
+      if (pl >= 0 && pend == i) Tm |= 1ull << l;
+      if (pl >= 0 && pend == i + 2 && pend - w0 < 64) Rm |= 1ull << l;
+      if ((ch >> l) & 1) {
+        const int prev = pl >= 0 ? pend : anchor_in;
+        const int blim = i - prev < tc[l] ? i - prev : tc[l];
+        f_cand[l] = tc[l];
+        f_len[l] = len[l];
+        f_bk[l] = bkr[l] < blim ? bkr[l] : blim;
+        if (bkr[l] == kRegBack && blim > kRegBack) ok = false;        // long catch-up
+        if (len[l] == kRegLen && i + kRegLen < b.mlim) ok = false;    // length not final
+        if (i + len[l] >= b.mfl1) ok = false;                         // last literals follow
+      }
+    }
+    if (mode == POSTMATCH) { Tm |= 4; Rm |= 1; }
+    const uint64_t ins = Mv | Rm;
+    for (int l = 0; l < 64; ++l)                                      // a window-local candidate
+      if (((Mv >> l) & 1) && (eq[l] & ins & below(l))) ok = false;
+    if (mode == SEARCH) {                                             // strides above 1 reached
+      const int x1 = ch ? __builtin_ctzll(ch) : 63;
+      if (b.cnt + x1 > 64) ok = false;
+    }
+    if (ok) {
+      fast_done = true;
+      b.fastwin++;
+      INS = ins;
+      chosen = ch;
+      for (int l = 0; l < 64; ++l)
+        if ((ch >> l) & 1) { L_cand[l] = f_cand[l]; L_len[l] = f_len[l]; L_bk[l] = f_bk[l]; }
+      const int cl = ch ? 63 - __builtin_clzll(ch) : -1;
+      const int end = cl >= 0 ? cl + len[cl] : -1;                    // lane after the last match
+      if (cl >= 0) anchor = w0 + end;
+      if (cl >= 0 && end >= 64) {
+        b.ip = w0 + end;
+        next_mode = POSTMATCH;
+      } else {
+        b.ip = w0 + 64;
+        next_mode = SEARCH;
+        const int tl = Tm ? 63 - __builtin_clzll(Tm) : -1;            // last re-tested lane
+        b.cnt = tl >= 0 ? 63 - tl : b.cnt + 64;
+      }
+    }
+  }
+
+  if (!fast_done) {
   // three-state machine, as in the kernel
   enum { S_SEARCH = 0, S_FOUND = 1, S_POST = 2 };
   int state = S_SEARCH;
@@ -229,6 +311,7 @@ Status window(Block &b, int w0, Mode mode, int forced_cand, Mode &next_mode) {
     }
   }
 
+  }  // !fast_done
   // ---- table update: every inserted lane, the latest position per hash wins
   if (st != LAST)
     for (int l = 0; l < 64; ++l)
@@ -275,7 +358,7 @@ Status window(Block &b, int w0, Mode mode, int forced_cand, Mode &next_mode) {
 }  // namespace
 
 extern "C" int sim_lz4_window_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap,
-                                    long *stats /* 5 counters, may be null */) {
+                                    long *stats /* 6 counters, may be null */) {
   static thread_local Block b;
   b.src = src;
   b.n = n;
@@ -284,7 +367,7 @@ extern "C" int sim_lz4_window_block(const uint8_t *src, int n, uint8_t *dst, int
   b.mlim = n - kLastLiterals;
   b.olimit = dst_cap;
   b.ip = 1; b.cnt = 0; b.anchor = 0; b.op = 0;
-  b.windows = b.generic = b.inwin = b.longfwd = b.longback = 0;
+  b.windows = b.generic = b.inwin = b.longfwd = b.longback = b.fastwin = 0;
   memset(b.table, 0, sizeof b.table);
   if (n >= kMFLimit + 1) {  // LZ4_minLength (lz4.c:876)
     Mode mode = SEARCH;
@@ -324,7 +407,7 @@ extern "C" int sim_lz4_window_block(const uint8_t *src, int n, uint8_t *dst, int
   op += lastRun;
   if (stats) {
     stats[0] = b.windows; stats[1] = b.generic; stats[2] = b.inwin;
-    stats[3] = b.longfwd; stats[4] = b.longback;
+    stats[3] = b.longfwd; stats[4] = b.longback; stats[5] = b.fastwin;
   }
   return op;
 }

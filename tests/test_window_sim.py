@@ -30,7 +30,7 @@ def _both(sim, oracle_mod, data):
     src = C.create_string_buffer(bytes(data), max(1, n))
     d1 = C.create_string_buffer(n + 64)
     d2 = C.create_string_buffer(n + 64)
-    stats = (C.c_long * 5)()
+    stats = (C.c_long * 6)()
     c1 = sim.sim_lz4_window_block(src, n, d1, n - 1, stats)
     c2 = oracle_mod.lib().or_lz4_compress_block(src, n, d2, n - 1, 1)
     return c1, d1.raw[:max(c1, 0)], c2, d2.raw[:max(c2, 0)], list(stats)
@@ -74,7 +74,7 @@ def _inputs(seed, count):
 
 
 def test_window_parse_is_byte_identical_to_the_oracle(sim, oracle_mod):
-    tot = [0] * 5
+    tot = [0] * 6
     for i, data in enumerate(_inputs(1, 400)):
         c1, b1, c2, b2, st = _both(sim, oracle_mod, data)
         assert c1 == c2 and b1 == b2, (i, len(data), c1, c2)

@@ -34,11 +34,13 @@ struct Ctx {
   hipStream_t d_last[4] = {nullptr, nullptr, nullptr, nullptr};  // stream of the last user
   hipEvent_t d_done[4] = {nullptr, nullptr, nullptr, nullptr};  // recorded after the last use
   bool d_used[4] = {false, false, false, false};
-  // the split CRC's partial registers (64 KiB), one buffer per caller stream: calls on
-  // different streams never meet, so no event or allocation orders them
+  // CRC partial registers (the split CRC's chunks, the compress epilogue's block
+  // registers), one grow-only buffer per caller stream: calls on different streams never
+  // meet, so no event or allocation orders them
   static constexpr int kCrcStreams = 32;
   hipStream_t crc_stream[kCrcStreams] = {};
   uint32_t *crc_buf[kCrcStreams] = {};
+  size_t crc_cap[kCrcStreams] = {};
   int crc_streams = 0;
   // small device descriptor buffer
   uint8_t *d_desc = nullptr;
@@ -59,8 +61,9 @@ constexpr int kScratchRegions = 4;
 // region has to grow), release marks the end of this use on `s`.
 int scratch_acquire(Ctx *c, int which, size_t bytes, hipStream_t s);
 int scratch_release(Ctx *c, int which, hipStream_t s);
-// 64 KiB of device words private to (this thread, stream s); nullptr with the error set
-uint32_t *crc_scratch(Ctx *c, hipStream_t s);
+// `bytes` (at least 64 KiB) of device words private to (this thread, stream s); nullptr
+// with the error set
+uint32_t *crc_scratch(Ctx *c, hipStream_t s, size_t bytes = 65536);
 
 // Device-resident CRC tables for `device` (uploaded once per device).  kind selects the
 // polynomial: kCrcKind32C (CRC-32C, crc32c.c) or kCrcKind32 (CRC-32/zlib, rdcrc32.h).

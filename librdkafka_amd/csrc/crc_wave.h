@@ -1,0 +1,85 @@
+// crc_wave.h -- CRC32C of a byte range by ONE wavefront, for the compress epilogue.
+//
+// rd_kafka_msgset_writer_calc_crc_v2 (rdkafka_msgset_writer.c:1229-1246) runs over the
+// finished batch after compression.  Here every compressed block's CRC is taken by the
+// wave that has just written it (the bytes are still in its L2), as a RAW register
+// (zero initial value, no final inversion: then the CRC is GF(2)-linear in the data,
+// leading zero bytes do not matter and pieces combine by shifting, crc32c.c:144-231), and
+// the frame assembler combines header, blocks and end mark into the batch's CRC.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "crc32c_tables.h"
+#include "lz4_device.h"
+
+namespace rdk {
+
+typedef __attribute__((address_space(3))) uint32_t crcw_lds_u32;
+
+// multiply in GF(2)[x]/P, reflected (bit 31 = x^0)
+__device__ __forceinline__ uint32_t crcw_mul(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+#pragma unroll 4
+  for (int i = 0; i < 32; ++i) {
+    if (a & m) p ^= b;
+    m >>= 1;
+    b = (b & 1u) ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+
+// x^(8*nbytes) mod P from the x^(2^k) table (k = 0..63)
+__device__ __forceinline__ uint32_t crcw_xpow8n(uint32_t nbytes, const uint32_t *__restrict__ x2n) {
+  uint32_t p = 1u << 31;
+  int k = 3;
+  for (uint32_t n = nbytes; n; n >>= 1, ++k)
+    if (n & 1u) p = crcw_mul(x2n[k], p);
+  return p;
+}
+
+// the raw register advanced over nbytes zero bytes
+__device__ __forceinline__ uint32_t crcw_shift(uint32_t r, uint32_t nbytes,
+                                               const uint32_t *__restrict__ x2n) {
+  return nbytes ? crcw_mul(crcw_xpow8n(nbytes, x2n), r) : r;
+}
+
+// 256 dwords of the byte table T0 (raw CRC of one byte) into LDS, by one wave
+__device__ __forceinline__ void crcw_load_t0(crcw_lds_u32 *t0, const uint32_t *__restrict__ tabs,
+                                             int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t0[lane + 64 * j] = tabs[lane + 64 * j];
+  asm volatile("" ::: "memory");
+}
+
+// Raw CRC32C register (zero in, no inversion) of the `len` bytes at `addr`, whole wave;
+// the result is wave-uniform.  Lane l takes the l-th piece of P = ceil(len/64) bytes
+// counted from the END of the range (the front lanes' missing bytes are leading zeros),
+// byte by byte through T0; the 64 registers combine in a shift-and-xor scan.
+__device__ __forceinline__ uint32_t wave_crc_raw(uintptr_t addr, uint32_t len,
+                                                 const crcw_lds_u32 *t0,
+                                                 const uint32_t *__restrict__ x2n, int lane) {
+  if (!len) return 0u;
+  const uint32_t P = (len + 63u) / 64u;
+  const int64_t hi = int64_t(len) - int64_t(63 - lane) * int64_t(P);  // piece = [hi - P, hi)
+  const int64_t lo = hi - int64_t(P);
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < P; ++k) {
+    const int64_t at = lo + int64_t(k);
+    const uint32_t b = at >= 0 ? ldb(addr + uint64_t(at)) : 0u;
+    r = t0[(r ^ b) & 0xFFu] ^ (r >> 8);
+  }
+  uint32_t X = uint32_t(__builtin_amdgcn_readfirstlane(int(crcw_xpow8n(P, x2n))));  // x^(8P)
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = uint32_t(__shfl_up(int(r), d));
+    const uint32_t m = crcw_mul(X, t);
+    if (lane >= d) r ^= m;
+    X = crcw_mul(X, X);
+  }
+  return uint32_t(__builtin_amdgcn_readlane(int(r), 63));
+}
+
+}  // namespace rdk

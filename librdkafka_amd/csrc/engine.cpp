@@ -208,21 +208,35 @@ int scratch_release(Ctx *c, int which, hipStream_t s) {
   return 0;
 }
 
-uint32_t *crc_scratch(Ctx *c, hipStream_t s) {
+uint32_t *crc_scratch(Ctx *c, hipStream_t s, size_t bytes) {
+  if (bytes < 65536) bytes = 65536;
+  int slot = -1;
   for (int i = 0; i < c->crc_streams; ++i)
-    if (c->crc_stream[i] == s) return c->crc_buf[i];
-  int slot = c->crc_streams;
-  if (slot == Ctx::kCrcStreams) {
-    // more streams than slots: recycle the oldest once its stream has drained
-    slot = 0;
-    if (hipStreamSynchronize(c->crc_stream[0]) != hipSuccess) (void)hipGetLastError();
-  } else {
-    uint8_t *p = nullptr;
-    if (dev_alloc(&p, 65536)) return nullptr;
-    c->crc_buf[slot] = reinterpret_cast<uint32_t *>(p);
-    c->crc_streams++;
+    if (c->crc_stream[i] == s) slot = i;
+  if (slot < 0) {
+    if (c->crc_streams < Ctx::kCrcStreams) {
+      slot = c->crc_streams++;
+      c->crc_buf[slot] = nullptr;
+      c->crc_cap[slot] = 0;
+    } else {  // more streams than slots: recycle the oldest once its stream has drained
+      slot = 0;
+      if (hipStreamSynchronize(c->crc_stream[0]) != hipSuccess) (void)hipGetLastError();
+    }
+    c->crc_stream[slot] = s;
   }
-  c->crc_stream[slot] = s;
+  if (c->crc_cap[slot] < bytes) {
+    if (c->crc_buf[slot]) {  // kernels of earlier calls on this stream may still use it
+      if (hipStreamSynchronize(s) != hipSuccess) (void)hipGetLastError();
+      (void)hipFree(c->crc_buf[slot]);
+      c->crc_buf[slot] = nullptr;
+      c->crc_cap[slot] = 0;
+    }
+    uint8_t *p = nullptr;
+    const size_t n = grow(0, bytes);
+    if (dev_alloc(&p, n)) return nullptr;
+    c->crc_buf[slot] = reinterpret_cast<uint32_t *>(p);
+    c->crc_cap[slot] = n;
+  }
   return c->crc_buf[slot];
 }
 

@@ -43,7 +43,9 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "crc_wave.h"
 #include "lz4_device.h"
+#include "lz4_engine.h"
 #include "lz4_wave.h"
 
 namespace rdk {
@@ -853,6 +855,22 @@ __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table,
   return op + int(last);
 }
 
+// Raw CRC32C register of one block in stream form (LE32 size word, then the payload the
+// wave has just written or, for a stored block, the source bytes).  The byte table goes
+// into the front of the block's LDS, which is dead once the block is compressed.
+__device__ __forceinline__ uint32_t block_stream_crc(uint32_t w, uintptr_t payload, uint32_t plen,
+                                                     crcw_lds_u32 *t0, const FuseCrc &fuse,
+                                                     int lane) {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the block's own stores are done
+  crcw_load_t0(t0, fuse.t0, lane);
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r = t0[(r ^ (w >> (8 * j))) & 0xFFu] ^ (r >> 8);
+  const uint32_t c = crcw_shift(r, plen, fuse.x2n) ^ wave_crc_raw(payload, plen, t0, fuse.x2n, lane);
+  asm volatile("" ::: "memory");
+  return c;
+}
+
 // One wavefront per block.  Block k of frame f goes to the worst-case slot
 // at out_offs[f] + 7 + k*kSlot as [LE32 size word][payload]; a block stored
 // raw gets only its size word (payload is taken from the input later).
@@ -860,7 +878,7 @@ template <bool WINDOWS>
 __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
-    const uint64_t *__restrict__ out_offs, uint32_t n, int accel) {
+    const uint64_t *__restrict__ out_offs, uint32_t n, int accel, FuseCrc fuse) {
   // the source ring (windowed engine) sits in front of the hash table
   constexpr uint32_t kRingLds = WINDOWS ? kRingBytes : 0u;
   __shared__ __attribute__((aligned(16))) uint8_t lds_mem[kRingLds + (2u << kHashLog)];
@@ -892,22 +910,38 @@ __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
         csize = WINDOWS ? window_block(src, int(bn), slot + 4u, table, (lds_u32 *)lds_mem, lane)
                         : compress_block(src, int(bn), slot + 4u, accel, table, lane);
       }
+      const uint32_t w = csize ? uint32_t(csize) : (bn | 0x80000000u);  // LZ4F_makeBlock
       if (lane == 0) {
-        const uint32_t w = csize ? uint32_t(csize) : (bn | 0x80000000u);  // LZ4F_makeBlock
         stb(slot, w & 0xFFu); stb(slot + 1, (w >> 8) & 0xFFu);
         stb(slot + 2, (w >> 16) & 0xFFu); stb(slot + 3, w >> 24);
       }
+      if (fuse.block_crc && k < uint32_t(kEncMaxItems))
+        fuse.block_crc[size_t(f) * kEncMaxItems + k] =
+            block_stream_crc(w, csize ? slot + 4u : src, csize ? uint32_t(csize) : bn,
+                             (crcw_lds_u32 *)lds_mem, fuse, lane);
     }
   }
 }
 
 // One workgroup per frame: header (lz4frame.c:671-701), size words, blocks
 // slid down from their slots (raw blocks copied from the input), end mark.
+// FIN: the frame sits 61 bytes into a MsgVersion 2 batch slot and the workgroup also
+// finishes the batch (see FuseCrc): codec choice, header, CRC32C from the block registers.
+template <bool FIN>
 __global__ __launch_bounds__(256) void lz4f_assemble_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
-    uint32_t *__restrict__ out_lens, uint32_t n) {
+    uint32_t *__restrict__ out_lens, uint32_t n, FuseCrc fuse) {
+  constexpr uint32_t kHdr = 61;  // RD_KAFKAP_MSGSET_V2_SIZE (rdkafka_proto.h:540)
+  __shared__ uint32_t t0_mem[FIN ? 256 : 1];
+  __shared__ uint32_t s_sz[FIN ? 64 : 1];
+  __shared__ uint32_t s_term[FIN ? 65 : 1];
   const int t = threadIdx.x;
+  if (FIN) {
+    t0_mem[t] = fuse.t0[t];
+    __syncthreads();
+  }
+  crcw_lds_u32 *t0 = (crcw_lds_u32 *)t0_mem;
   for (uint32_t f = blockIdx.x; f < n; f += gridDim.x) {
     const uint32_t len = in_lens[f];
     const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
@@ -946,13 +980,68 @@ __global__ __launch_bounds__(256) void lz4f_assemble_kernel(
       if (t == 0) {
         stb(ob + pos, w & 0xFFu); stb(ob + pos + 1, (w >> 8) & 0xFFu);
         stb(ob + pos + 2, (w >> 16) & 0xFFu); stb(ob + pos + 3, w >> 24);
+        if (FIN && k < 64u) s_sz[k] = sz;
       }
       __syncthreads();
       pos += 4u + sz;
     }
+    const uint32_t flen = uint32_t(pos + 4u);
     if (t == 0) {
       stb(ob + pos, 0); stb(ob + pos + 1, 0); stb(ob + pos + 2, 0); stb(ob + pos + 3, 0);
-      out_lens[f] = uint32_t(pos + 4u);
+      out_lens[f] = flen;
+    }
+    if (FIN) {
+      // ---- rd_kafka_msgset_writer_compress's verdict (rdkafka_msgset_writer.c:1179-1187)
+      // and finalize_MessageSet_v2_header (:1251-1295)
+      const uintptr_t bo = ob - kHdr;                     // the batch slot
+      const uintptr_t hdr = ib - kHdr;                    // the header the writer left
+      const bool compressed = flen <= len;
+      const uint32_t payload = compressed ? flen : len;
+      __syncthreads();                                    // the frame is complete
+      if (!compressed)                                    // keep the records plain
+        for (uint32_t k = t; k < len; k += 256u) stb(ob + k, ldb(ib + k));
+      if (uint32_t(t) < kHdr) {
+        uint32_t v = ldb(hdr + uint32_t(t));
+        const uint32_t length = kHdr + payload - 12u;
+        if (t >= 8 && t < 12) v = (length >> (8u * (3u - (uint32_t(t) - 8u)))) & 0xFFu;
+        if (t == 22 && compressed) v |= 3u;               // Attributes |= RD_KAFKA_COMPRESSION_LZ4
+        if (t >= 17 && t < 21) v = 0;
+        stb(bo + uint32_t(t), v);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      // ---- calc_crc_v2 (:1229-1246) over [21, 61 + payload) without re-reading the frame:
+      // header bytes and LZ4F header through the byte table, then one term per block
+      uint32_t crc;
+      if (compressed && nb <= 64u) {
+        if (uint32_t(t) < nb) {
+          uint32_t after = 4u;                            // the end mark
+          for (uint32_t j = uint32_t(t) + 1u; j < nb; ++j) after += 4u + s_sz[j];
+          s_term[t] = crcw_shift(fuse.block_crc[size_t(f) * 64u + uint32_t(t)], after, fuse.x2n);
+        } else if (t == 64) {
+          uint32_t r = ~0u;                               // crc32c()'s initial register
+          for (uint32_t k = 21; k < kHdr + 7u; ++k) r = t0[(r ^ ldb(bo + k)) & 0xFFu] ^ (r >> 8);
+          s_term[64] = crcw_shift(r, flen - 7u, fuse.x2n);
+        }
+        __syncthreads();
+        uint32_t r = s_term[64];
+        for (uint32_t k = 0; k < nb; ++k) r ^= s_term[k];
+        crc = ~r;
+      } else {
+        // plain records, or more blocks than registers were kept for: the first wavefront
+        // runs over the finished bytes
+        crc = 0;
+        if (t < 64) {
+          const uint32_t total = kHdr - 21u + payload;
+          crc = ~(crcw_shift(~0u, total, fuse.x2n) ^ wave_crc_raw(bo + 21u, total, t0, fuse.x2n, t));
+        }
+      }
+      if (t == 0) {
+        stb(bo + 17, crc >> 24); stb(bo + 18, (crc >> 16) & 0xFFu);
+        stb(bo + 19, (crc >> 8) & 0xFFu); stb(bo + 20, crc & 0xFFu);
+        fuse.batch_lens[f] = kHdr + payload;
+        fuse.crcs[f] = crc;
+      }
     }
     __syncthreads();
   }
@@ -965,13 +1054,15 @@ size_t lz4f_compress_bound(size_t len) {
 
 void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
-                          uint32_t n, hipStream_t s);
+                          uint32_t n, hipStream_t s, const FuseCrc *fuse = nullptr);
 
 int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
                          const uint32_t *d_in_lens, uint8_t *d_out, const uint64_t *d_out_offs,
-                         uint32_t *d_out_lens, uint32_t n, int accel, hipStream_t s) {
+                         uint32_t *d_out_lens, uint32_t n, int accel, hipStream_t s,
+                         const FuseCrc *fuse) {
   (void)c;
   if (!n) return 0;
+  const FuseCrc fz = fuse ? *fuse : FuseCrc();
   uint64_t items = uint64_t(n) * kEncMaxItems;
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
   // RDK_HIP_LZ4_EXACT_SEQ=1 keeps the sequence-at-a-time engine for acceleration 1 too
@@ -979,26 +1070,30 @@ int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
   static const bool seq_only = getenv("RDK_HIP_LZ4_EXACT_SEQ") && atoi(getenv("RDK_HIP_LZ4_EXACT_SEQ"));
   if (accel == 1 && !seq_only)
     hipLaunchKernelGGL(lz4_compress_blocks_kernel<true>, dim3(grid), dim3(64), 0, s, d_in,
-                       d_in_offs, d_in_lens, d_out, d_out_offs, n, accel);
+                       d_in_offs, d_in_lens, d_out, d_out_offs, n, accel, fz);
   else
     hipLaunchKernelGGL(lz4_compress_blocks_kernel<false>, dim3(grid), dim3(64), 0, s, d_in,
-                       d_in_offs, d_in_lens, d_out, d_out_offs, n, accel);
-  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s);
+                       d_in_offs, d_in_lens, d_out, d_out_offs, n, accel, fz);
+  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s, fuse);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;
 }
 
 void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
-                          uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL(lz4f_assemble_kernel, dim3(n < 8192u ? n : 8192u), dim3(256), 0, s, d_in,
-                     d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n);
+                          uint32_t n, hipStream_t s, const FuseCrc *fuse) {
+  if (fuse)
+    hipLaunchKernelGGL(lz4f_assemble_kernel<true>, dim3(n < 8192u ? n : 8192u), dim3(256), 0, s,
+                       d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, *fuse);
+  else
+    hipLaunchKernelGGL(lz4f_assemble_kernel<false>, dim3(n < 8192u ? n : 8192u), dim3(256), 0, s,
+                       d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, FuseCrc());
 }
 
 int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
                               const uint32_t *d_in_lens, uint8_t *d_out,
                               const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
-                              hipStream_t s);
+                              hipStream_t s, const FuseCrc *fuse);
 int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, int level, hipStream_t s);
@@ -1027,7 +1122,8 @@ RDK_API int rdk_hip_lz4f_compress(const void *d_in, const uint64_t *d_in_offs,
                                  static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n, level, s);
   const int accel = level < 0 ? -level + 1 : 1;  // LZ4F_compressBlock, lz4frame.c:766
   return lz4f_compress_device(c, static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
-                              static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n, accel, s);
+                              static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n, accel, s,
+                              nullptr);
 }
 
 RDK_API int rdk_hip_lz4f_compress_fast(const void *d_in, const uint64_t *d_in_offs,
@@ -1041,5 +1137,5 @@ RDK_API int rdk_hip_lz4f_compress_fast(const void *d_in, const uint64_t *d_in_of
     return set_error(RDK_HIP_E_INVAL, "null pointer");
   return lz4f_compress_fast_device(static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
                                    static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n,
-                                   static_cast<hipStream_t>(stream));
+                                   static_cast<hipStream_t>(stream), nullptr);
 }

@@ -31,14 +31,16 @@
 #include <hip/hip_runtime.h>
 
 #include "common.h"
+#include "crc_wave.h"
 #include "lz4_device.h"
+#include "lz4_engine.h"
 #include "lz4_wave.h"
 
 namespace rdk {
 
 void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
-                          uint32_t n, hipStream_t s);
+                          uint32_t n, hipStream_t s, const FuseCrc *fuse);
 
 namespace {
 
@@ -283,7 +285,7 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
 __global__ __launch_bounds__(64) void lz4_fast_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
-    const uint64_t *__restrict__ out_offs, uint32_t n) {
+    const uint64_t *__restrict__ out_offs, uint32_t n, FuseCrc fuse) {
   __shared__ __attribute__((aligned(16))) uint16_t table_mem[1u << kFastHashLog];
   lds_u16 *table = (lds_u16 *)table_mem;
   const int lane = threadIdx.x;
@@ -310,10 +312,25 @@ __global__ __launch_bounds__(64) void lz4_fast_blocks_kernel(
         asm volatile("" ::: "memory");
         csize = fast_block(src, int(bn), slot + 4u, table, lane);
       }
+      const uint32_t w = csize ? uint32_t(csize) : (bn | 0x80000000u);  // LZ4F_makeBlock
       if (lane == 0) {
-        const uint32_t w = csize ? uint32_t(csize) : (bn | 0x80000000u);  // LZ4F_makeBlock
         stb(slot, w & 0xFFu); stb(slot + 1, (w >> 8) & 0xFFu);
         stb(slot + 2, (w >> 16) & 0xFFu); stb(slot + 3, w >> 24);
+      }
+      if (fuse.block_crc && k < uint32_t(kFastMaxItems)) {
+        // the compress epilogue's CRC (crc_wave.h): raw register of the block in stream
+        // form; the byte table goes into the hash table's LDS, dead until the next block
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        crcw_lds_u32 *t0 = (crcw_lds_u32 *)table_mem;
+        crcw_load_t0(t0, fuse.t0, lane);
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r = t0[(r ^ (w >> (8 * j))) & 0xFFu] ^ (r >> 8);
+        const uint32_t plen = csize ? uint32_t(csize) : bn;
+        fuse.block_crc[size_t(f) * kFastMaxItems + k] =
+            crcw_shift(r, plen, fuse.x2n) ^
+            wave_crc_raw(csize ? slot + 4u : src, plen, t0, fuse.x2n, lane);
+        asm volatile("" ::: "memory");
       }
     }
   }
@@ -324,13 +341,13 @@ __global__ __launch_bounds__(64) void lz4_fast_blocks_kernel(
 int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
                               const uint32_t *d_in_lens, uint8_t *d_out,
                               const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
-                              hipStream_t s) {
+                              hipStream_t s, const FuseCrc *fuse) {
   if (!n) return 0;
   const uint64_t items = uint64_t(n) * kFastMaxItems;
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
   hipLaunchKernelGGL(lz4_fast_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
-                     d_in_lens, d_out, d_out_offs, n);
-  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s);
+                     d_in_lens, d_out, d_out_offs, n, fuse ? *fuse : FuseCrc());
+  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s, fuse);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;
 }

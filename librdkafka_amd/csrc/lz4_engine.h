@@ -18,4 +18,19 @@ int lz4f_compress_host(Ctx *c, size_t len, int proper_hc, int level, void **out,
 int lz4f_decompress_host(Ctx *c, int proper_hc, uint8_t *in, size_t inlen, void **out,
                          size_t *outlen);
 
+// The compress epilogue's CRC (crc_wave.h): when block_crc is set, the block kernels store
+// the raw CRC32C register of every block in stream form (LE32 size word || payload) at
+// block_crc[frame * 64 + block] (blocks 0..63), and the frame assembler turns a frame that
+// sits 61 bytes into a MsgVersion 2 batch slot into the finished batch: header copied from
+// in front of the records with Length and the LZ4 codec bits set (or the records kept
+// plain when the frame is larger, rdkafka_msgset_writer.c:1179), CRC32C combined from the
+// header, the block registers and the end mark, stored at offset 17.
+struct FuseCrc {
+  uint32_t *block_crc = nullptr;   // n * 64 words of device scratch
+  const uint32_t *t0 = nullptr;    // byte table (256 words, device)
+  const uint32_t *x2n = nullptr;   // x^(2^k) mod P, k = 0..63 (device)
+  uint32_t *batch_lens = nullptr;  // out: 61 + payload bytes
+  uint32_t *crcs = nullptr;        // out: the stored CRC
+};
+
 }  // namespace rdk

@@ -20,7 +20,8 @@ int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const 
                           uint32_t n, int level, hipStream_t s);
 int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
                          const uint32_t *d_in_lens, uint8_t *d_out, const uint64_t *d_out_offs,
-                         uint32_t *d_out_lens, uint32_t n, int accel, hipStream_t s);
+                         uint32_t *d_out_lens, uint32_t n, int accel, hipStream_t s,
+                         const FuseCrc *fuse);
 int lz4f_decompress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
                            const uint32_t *d_in_lens, uint8_t *d_out,
                            const uint64_t *d_out_offs, const uint32_t *d_out_caps,
@@ -94,7 +95,7 @@ int lz4f_compress_host(Ctx *c, size_t len, int proper_hc, int level, void **out,
     if ((rc = lz4hc_compress_device(d_in, dd, d_len, d_out, dd + 1, d_olen, 1, level, c->stream)))
       return rc;
   } else if ((rc = lz4f_compress_device(c, d_in, dd, d_len, d_out, dd + 1, d_olen, 1, accel,
-                                        c->stream))) {
+                                        c->stream, nullptr))) {
     return rc;
   }
   RDK_HIP_CHECK(hipMemcpyAsync(c->h_desc + 32, d_olen, 4, hipMemcpyDeviceToHost, c->stream));

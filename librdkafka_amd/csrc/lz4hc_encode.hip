@@ -563,9 +563,10 @@ __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
   }
 }
 
+struct FuseCrc;
 void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
-                          uint32_t n, hipStream_t s);
+                          uint32_t n, hipStream_t s, const FuseCrc *fuse);
 
 // The hash/chain tables (kHcScratch bytes per wave) and the work-queue counter live in
 // the calling thread's kScratchHc region: calls on different streams are ordered by
@@ -588,7 +589,7 @@ int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const 
   RDK_HIP_CHECK(hipMemsetAsync(next_item, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(lz4hc_compress_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
                      d_in_lens, d_out, d_out_offs, n, attempts, p, next_item);
-  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s);
+  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s, nullptr);
   RDK_HIP_CHECK(hipGetLastError());
   return scratch_release(c, kScratchHc, s);
 }

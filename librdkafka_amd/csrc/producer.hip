@@ -9,13 +9,15 @@
 // filling slot -- the rd_slice gather the reference does before
 // rd_kafka_lz4_compress (rdkafka_lz4.c:390) -- and a full slot is launched as
 //
-//   H2D -> LZ4F compress of every batch's records (exact or fast engine)
-//       -> v2_finalize_kernel: header copy, codec choice exactly as
-//          rd_kafka_msgset_writer_compress (rdkafka_msgset_writer.c:1179:
-//          a frame larger than the records is thrown away), Attributes |= LZ4
-//          (:1187), Length = size-12 (:1265-1267)
-//       -> CRC32C finalize over [21, 12+Length), stored BE at 17 (:1229-1246)
-//       -> D2H of the finished batches
+//   H2D -> rdk_hip_msgset_v2_finalize, two kernels:
+//          LZ4F block compress of every batch's records (exact or fast engine), each
+//          wave also leaving the raw CRC32C register of the block it wrote;
+//          frame assembly + codec choice exactly as rd_kafka_msgset_writer_compress
+//          (rdkafka_msgset_writer.c:1179: a frame larger than the records is thrown
+//          away), Attributes |= LZ4 (:1187), Length = size-12 (:1265-1267), and the
+//          CRC32C over [21, 12+Length) combined from the block registers, stored BE
+//          at 17 (:1229-1246) -- no separate CRC pass over the frame
+//       -> the finished batches packed into pinned host memory
 //
 // on the slot's stream, so slot k+1's copies overlap slot k's kernels.
 // poll() hands finished batches back in submission order.
@@ -28,43 +30,11 @@
 
 #include "common.h"
 #include "lz4_device.h"
+#include "lz4_engine.h"
 
 namespace rdk {
 
 constexpr uint32_t kV2Hdr = 61;       // RD_KAFKAP_MSGSET_V2_SIZE (rdkafka_proto.h:540)
-constexpr uint32_t kV2OfLength = 8;   // RD_KAFKAP_MSGSET_V2_OF_Length
-constexpr uint32_t kV2OfAttr = 21;    // RD_KAFKAP_MSGSET_V2_OF_Attributes
-constexpr uint32_t kCodecLz4 = 3;     // RD_KAFKA_COMPRESSION_LZ4 (rdkafka_msg.h:48)
-
-// One workgroup per batch: out[out_off] = header, then either the frame the
-// compressor left at out_off+61 or (frame longer than the records) the
-// records themselves.
-__global__ __launch_bounds__(256) void v2_finalize_kernel(
-    const uint8_t *__restrict__ in, const uint64_t *__restrict__ rec_offs,
-    const uint32_t *__restrict__ rec_lens, uint8_t *__restrict__ out,
-    const uint64_t *__restrict__ out_offs, const uint32_t *__restrict__ frame_lens,
-    uint32_t *__restrict__ batch_lens, uint32_t n) {
-  const uint32_t t = threadIdx.x;
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    const uint8_t *rec = in + rec_offs[i];
-    const uint8_t *hdr = rec - kV2Hdr;
-    uint8_t *o = out + out_offs[i];
-    const uint32_t len = rec_lens[i], flen = frame_lens[i];
-    const bool compressed = flen <= len;
-    const uint32_t payload = compressed ? flen : len;
-    if (!compressed)  // the frame slot holds >= len bytes, so the records fit
-      for (uint32_t k = t; k < len; k += blockDim.x) o[kV2Hdr + k] = rec[k];
-    if (t < kV2Hdr) {
-      uint32_t v = hdr[t];
-      const uint32_t length = kV2Hdr + payload - 12u;
-      if (t >= kV2OfLength && t < kV2OfLength + 4u) v = (length >> (8u * (3u - (t - kV2OfLength)))) & 0xFFu;
-      if (t == kV2OfAttr + 1u && compressed) v |= kCodecLz4;  // Attributes |= codec (low byte, BE)
-      if (t >= 17u && t < 21u) v = 0;  // CRC slot, filled by the CRC pass
-      o[t] = uint8_t(v);
-    }
-    if (t == 0) batch_lens[i] = kV2Hdr + payload;
-  }
-}
 
 namespace {
 
@@ -85,6 +55,14 @@ struct Slot {
 }  // namespace
 
 size_t lz4f_compress_bound(size_t len);
+int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
+                         const uint32_t *d_in_lens, uint8_t *d_out, const uint64_t *d_out_offs,
+                         uint32_t *d_out_lens, uint32_t n, int accel, hipStream_t s,
+                         const FuseCrc *fuse);
+int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
+                              const uint32_t *d_in_lens, uint8_t *d_out,
+                              const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
+                              hipStream_t s, const FuseCrc *fuse);
 
 }  // namespace rdk
 
@@ -168,28 +146,26 @@ RDK_API int rdk_hip_msgset_v2_finalize(const void *d_in, const uint64_t *d_rec_o
   if (mode != RDK_HIP_PRODUCER_EXACT && mode != RDK_HIP_PRODUCER_FAST)
     return set_error(RDK_HIP_E_INVAL, "bad mode %d", mode);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // frame i goes 61 bytes into batch i's output slot; the offsets array is derived on the
-  // device so the caller passes one array
-  int rc;
-  {
-    // frame offsets = out_offs + 61: reuse d_batch_lens' neighbour is not possible, so the
-    // compressors take a byte-shifted base instead (same offsets, base + 61)
-    uint8_t *fbase = static_cast<uint8_t *>(d_out) + kV2Hdr;
-    if (mode == RDK_HIP_PRODUCER_FAST)
-      rc = rdk_hip_lz4f_compress_fast(d_in, d_rec_offs, d_rec_lens, fbase, d_out_offs, d_frame_lens,
-                                      n, stream);
-    else
-      rc = rdk_hip_lz4f_compress(d_in, d_rec_offs, d_rec_lens, fbase, d_out_offs, d_frame_lens, n,
-                                 0, stream);
-  }
-  if (rc) return rc;
-  hipLaunchKernelGGL(v2_finalize_kernel, dim3(n < 4096u ? n : 4096u), dim3(256), 0, s,
-                     static_cast<const uint8_t *>(d_in), d_rec_offs, d_rec_lens,
-                     static_cast<uint8_t *>(d_out), d_out_offs, d_frame_lens, d_batch_lens, n);
-  RDK_HIP_CHECK(hipGetLastError());
-  // CRC32C over [21, 12+Length) of each finished batch, stored BE at 17
-  return rdk_hip_msgset_v2_crc(d_out, d_out_offs, d_out_caps, d_crcs, n, RDK_HIP_V2_CRC_FINALIZE,
-                               stream);
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  (void)d_out_caps;  // slots are sized by the caller from rdk_hip_lz4f_compress_bound()
+  // Two launches: the block kernel, which also leaves the raw CRC32C register of every
+  // block it writes (crc_wave.h), and the frame assembler, which also makes the writer's
+  // codec choice, finishes the header and combines the batch's CRC from those registers.
+  // Frame i goes 61 bytes into batch i's output slot: same offsets on a shifted base.
+  FuseCrc fz;
+  fz.block_crc = crc_scratch(c, s, size_t(n) * 64 * sizeof(uint32_t));
+  if (!fz.block_crc) return RDK_HIP_E_NOMEM;
+  fz.t0 = crc_tables_dev(c->device);
+  fz.x2n = crc_x2n_dev(c->device);
+  fz.batch_lens = d_batch_lens;
+  fz.crcs = d_crcs;
+  uint8_t *fbase = static_cast<uint8_t *>(d_out) + kV2Hdr;
+  if (mode == RDK_HIP_PRODUCER_FAST)
+    return lz4f_compress_fast_device(static_cast<const uint8_t *>(d_in), d_rec_offs, d_rec_lens,
+                                     fbase, d_out_offs, d_frame_lens, n, s, &fz);
+  return lz4f_compress_device(c, static_cast<const uint8_t *>(d_in), d_rec_offs, d_rec_lens, fbase,
+                              d_out_offs, d_frame_lens, n, 1, s, &fz);
 }
 
 namespace {

@@ -94,6 +94,13 @@ rd_kafka_resp_err_t rd_kafka_lz4_decompress(rd_kafka_broker_t *rkb, int proper_h
                                             int64_t Offset, char *inbuf, size_t inlen,
                                             void **outbuf, size_t *outlenp);
 
+/* How often each drop-in symbol above has been entered in this process, in the order
+ * crc32c, rd_slice_crc32c, rd_slice_crc32, rd_kafka_lz4_compress, rd_kafka_lz4_decompress.
+ * No counterpart in the reference: it lets an integration (a preload run, a relinked
+ * library) verify that the writer's and reader's call sites bind to this library.  With
+ * RDK_HIP_REPORT=1 in the environment the same counts are printed on stderr at exit. */
+void rdk_hip_dropin_calls(uint64_t out[5]);
+
 /* ------------------------------------------------------------- engine API */
 #define RDK_HIP_OK 0
 #define RDK_HIP_E_NODEV (-1)      /* no usable gfx950 device / code object */

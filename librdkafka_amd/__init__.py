@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "rdk_hip_gen_json", "rdk_hip_msgset_v2_sizes", "rdk_hip_msgset_v2_write",
     "rdk_hip_msgset_v2_index", "rd_slice_crc32", "rdk_hip_crc32_ranges",
     "rdk_hip_msgset_v01_crc", "rdk_hip_lz4f_decompress_noalloc", "rdk_hip_msgset_v2_finalize",
+    "rdk_hip_dropin_calls",
 )
 
 

@@ -38,6 +38,22 @@ static int crc_staged(Ctx *c, size_t len, uint32_t init, uint32_t *out, int kind
   return 0;
 }
 
+// how often each drop-in symbol was entered (rdk_hip_dropin_calls)
+static std::atomic<uint64_t> g_calls[5];
+enum { CALL_CRC32C = 0, CALL_SLICE_CRC32C, CALL_SLICE_CRC32, CALL_LZ4C, CALL_LZ4D };
+
+// RDK_HIP_REPORT=1: one line on stderr at process exit with the call counts, so a preload
+// run of an unmodified program shows that its call sites reached the engine
+__attribute__((destructor)) static void report_calls() {
+  const char *e = getenv("RDK_HIP_REPORT");
+  if (!e || !atoi(e)) return;
+  fprintf(stderr, "librdkafka_hip: calls crc32c=%llu rd_slice_crc32c=%llu rd_slice_crc32=%llu "
+                  "rd_kafka_lz4_compress=%llu rd_kafka_lz4_decompress=%llu\n",
+          (unsigned long long)g_calls[0].load(), (unsigned long long)g_calls[1].load(),
+          (unsigned long long)g_calls[2].load(), (unsigned long long)g_calls[3].load(),
+          (unsigned long long)g_calls[4].load());
+}
+
 static Ctx *ctx_or_die(const char *who) {
   Ctx *c = ctx();
   if (!c) fatal(who);
@@ -86,7 +102,12 @@ using namespace rdk;
 
 RDK_API void crc32c_global_init(void) { (void)ctx_or_die("crc32c_global_init"); }
 
+RDK_API void rdk_hip_dropin_calls(uint64_t out[5]) {
+  for (int i = 0; i < 5; ++i) out[i] = g_calls[i].load();
+}
+
 RDK_API uint32_t crc32c(uint32_t crc, const void *buf, size_t len) {
+  g_calls[CALL_CRC32C]++;
   Ctx *c = ctx_or_die("crc32c");
   if (len == 0) return crc;  // pre/post inversions cancel (crc32c.c:102,133)
   if (ensure_host(c, len)) fatal("crc32c: pinned staging");
@@ -110,6 +131,7 @@ static uint32_t slice_crc(rd_slice_t *slice, int kind, const char *who) {
 }
 
 RDK_API uint32_t rd_slice_crc32c(rd_slice_t *slice) {
+  g_calls[CALL_SLICE_CRC32C]++;
   return slice_crc(slice, kCrcKind32C, "rd_slice_crc32c");
 }
 
@@ -117,6 +139,7 @@ RDK_API uint32_t rd_slice_crc32c(rd_slice_t *slice) {
 // (rdcrc32.h:93-131, WITH_ZLIB) -- the MsgVersion 0/1 check.crcs site
 // (rdkafka_msgset_reader.c:606)
 RDK_API uint32_t rd_slice_crc32(rd_slice_t *slice) {
+  g_calls[CALL_SLICE_CRC32]++;
   return slice_crc(slice, kCrcKind32, "rd_slice_crc32");
 }
 
@@ -125,6 +148,7 @@ RDK_API rd_kafka_resp_err_t rd_kafka_lz4_compress(rd_kafka_broker_t *rkb, int pr
                                                   int comp_level, rd_slice_t *slice,
                                                   void **outbuf, size_t *outlenp) {
   (void)rkb;
+  g_calls[CALL_LZ4C]++;
   *outbuf = nullptr;
   if (comp_level >= 10) {
     // LZ4HC optimal (lz4hc.c:1278, levels 10..12) is not implemented by the engine
@@ -158,6 +182,7 @@ RDK_API rd_kafka_resp_err_t rd_kafka_lz4_decompress(rd_kafka_broker_t *rkb, int 
                                                     void **outbuf, size_t *outlenp) {
   (void)rkb;
   (void)Offset;
+  g_calls[CALL_LZ4D]++;
   *outbuf = nullptr;
   Ctx *c = ctx();
   if (!c) return lz4_err(RDK_HIP_E_NODEV, "rd_kafka_lz4_decompress");

@@ -1,0 +1,20 @@
+# rocprofv3 evidence for one bench leg: kernel-trace stats, then FETCH_SIZE and WRITE_SIZE
+# in passes of their own (they cannot share one), summarised into profiles/r02/<leg>.json.
+#   usage: bash scripts/profile_r2.sh LEG "KERNEL_SUBSTR[,KERNEL_SUBSTR...]" bench.py-arguments...
+set -o pipefail
+LEG="$1"; KERNELS="$2"; shift 2
+R="$GRAFT_REPO_ROOT"
+O="$R/gpurun_out/prof_r2/$LEG"; rm -rf "$O"; mkdir -p "$O"
+cd /tmp && export TMPDIR=/tmp
+B="$R/bench.py --no-cpu-baseline --no-legs $*"
+echo "profile $LEG: trace"
+timeout -s KILL 240 rocprofv3 --kernel-trace --stats -T -f csv -d "$O/trace" -o t -- python3 $B > "$O/bench.json" 2> "$O/trace.err" || { echo "TRACE_FAILED $LEG"; tail -5 "$O/trace.err"; exit 1; }
+echo "profile $LEG: FETCH_SIZE"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -T -f csv -d "$O/pmc_fetch" -o t -- python3 $B > "$O/fetch.log" 2>&1 || { echo "FETCH_FAILED $LEG"; tail -5 "$O/fetch.log"; exit 1; }
+echo "profile $LEG: WRITE_SIZE"
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -T -f csv -d "$O/pmc_write" -o t -- python3 $B > "$O/write.log" 2>&1 || { echo "WRITE_FAILED $LEG"; tail -5 "$O/write.log"; exit 1; }
+mkdir -p "$R/gpurun_out/prof_r2/summaries"
+python3 "$R/scripts/profile_summary.py" "$O" "$LEG" "$KERNELS" "$R/gpurun_out/prof_r2/summaries/$LEG.json" || exit 1
+find "$O/trace" -name "*kernel_stats.csv" -exec cp {} "$R/gpurun_out/prof_r2/summaries/${LEG}_kernel_stats.csv" \;
+# the raw per-dispatch files are large: keep the summaries only
+rm -rf "$O/trace" "$O/pmc_fetch" "$O/pmc_write"

@@ -6,22 +6,25 @@
 // (lz4.c:789-1177, byU16 table, limitedOutput, dstCapacity = srcSize-1).
 //
 // One wavefront (one 64-thread workgroup) per independent 64 KiB block with
-// its own 8192-entry u16 hash table in LDS (16 KiB -> 10 blocks per CU).  The
-// greedy parse is emulated EXACTLY, so frames are byte-identical to the
-// reference's.  Two engines:
+// its own 8192-entry u16 hash table (16 KiB) and a 4 KiB source ring in LDS
+// (8 blocks per CU).  The greedy parse is emulated EXACTLY, so frames are
+// byte-identical to the reference's.  Two engines:
 //
 //  * window_block() (acceleration 1, i.e. compression.level 0..2): the parse runs
 //    in WINDOWS of 64 consecutive positions, one per lane.  Every lane loads its
 //    own 36 source bytes and its table candidate's 36 bytes once, verifies
-//    MINMATCH, measures the match (up to 28 bytes) and the catch-up (up to 4)
-//    from registers; a scalar walk then replays the sequential loop over those
-//    per-lane results: which positions are probed and inserted, the first
+//    MINMATCH, measures the match (up to 28 bytes, extended to 92 from the ring)
+//    and the catch-up (up to 4) from registers.  The sequential loop's path over
+//    those per-lane results -- which positions are probed and inserted, the first
 //    verifying probe, catch-up, ip-2 insertion and the immediate re-test after a
-//    match (lz4.c:1084-1134).  A candidate inserted earlier in the same window
-//    is found with a hash-equality mask over the lanes.  Several sequences per
-//    window cost two gathers, not a chain of dependent loads each; their bytes
-//    are emitted together at wave-prefix-sum positions.  Searches that outlast
-//    the stride-1 probes (lz4.c:896-905) continue in generic_search().
+//    match (lz4.c:1084-1134) -- is then found by pointer doubling over the
+//    verified lanes (the parallel walk); windows outside the conditions under
+//    which that shortcut is exact are replayed one sequence at a time (the scalar
+//    walk).  A candidate inserted earlier in the same window is found with a
+//    hash-equality mask over the lanes.  Several sequences per window cost two
+//    gathers, not a chain of dependent loads each; their bytes are emitted
+//    together at wave-prefix-sum positions.  Searches that outlast the stride-1
+//    probes (lz4.c:896-905) continue in generic_search().
 //
 //  * compress_block() (acceleration > 1, negative compression.level): one
 //    sequence at a time, every step through memory:

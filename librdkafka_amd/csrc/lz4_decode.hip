@@ -477,7 +477,8 @@ __device__ __forceinline__ int realcap_at(uint64_t cap, uint64_t at, uint32_t li
 }
 
 // independent blocks of regular frames: one wavefront per (frame, block)
-__global__ __launch_bounds__(64 * kDecWaves) void lz4f_blocks_kernel(
+__global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void
+lz4f_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs, uint8_t *out,
     const uint64_t *__restrict__ out_offs, const uint32_t *__restrict__ out_caps, uint32_t n,
     const FrameState *__restrict__ fs, BlockDesc *__restrict__ bd,

@@ -3,22 +3,26 @@
 // Included by lz4_decode.hip.  decode_block_fast() decodes one independent
 // block (LZ4_decompress_safe_usingDict with noDict, lz4.c:2307 ->
 // LZ4_decompress_generic lz4.c:1654-2068) without the per-sequence wave
-// round trips of the exact decoder:
+// round trips of the exact decoder.  The compressed block is cut into fixed
+// 64-byte segments; per segment:
 //
-//   1. DISCOVERY: the compressed block is cut into fixed 64-byte segments.
-//      For every byte position p of a segment, lane p%64 parses the
-//      sequence that WOULD start at p (token, literal / match length bytes,
-//      offset) from a 24-byte register window of its own, so a whole
-//      segment's candidates cost two loads and ~40 VALU.
-//   2. WALK: the true sequence chain is followed with one v_readlane per
-//      sequence (next start -> lane), scalar.  Each sequence "paints" the
-//      64-byte output chunk under construction: lane l of the chunk records
-//      where output byte oc+l comes from (an input position for literals,
-//      an earlier output position for matches).
-//   3. FLUSH: a complete chunk resolves its in-chunk match sources by
-//      pointer jumping (ds_bpermute, only when some offset < 64), fetches
-//      every byte at once (input, the wave's 8 KiB LDS history ring, or the
-//      already written output in HBM) and stores 64 contiguous bytes.
+//   1. DISCOVERY: for every byte position p of the segment, lane p%64 parses
+//      the sequence that WOULD start at p: token and literal length bytes from
+//      the 4 bytes at p, offset and match length bytes from a gather of the 4
+//      bytes behind the literals.  Branch-free, two loads, issued one and two
+//      segments ahead of their use.
+//   2. WALK: the true sequences are the orbit of the entry position under
+//      "next start"; it is marked by pointer doubling (5 levels cover the at
+//      most 22 sequences a segment can hold), in LDS, with no scalar chain.
+//   3. EXPANSION: the member lanes are in stream order, so a lane prefix sum over
+//      their lengths places every sequence in the output.  The segment's
+//      output is built in pieces of 64 bytes, lane per byte: sequence starts are
+//      scattered into a 64-byte LDS map and max-scanned, each lane fetches its
+//      sequence's fields (two ds_bpermute) and then its byte -- from the input
+//      (literals), the wave's LDS history ring, or the already written output
+//      in HBM; sources inside the piece are resolved by pointer jumping.  A
+//      fetched piece is written one piece later so its loads overlap the next
+//      piece's address work.
 //
 // The fast path only returns a result when the block is PROVABLY accepted
 // by the reference with this output: every condition under which
@@ -46,20 +50,17 @@ __device__ __forceinline__ rsrc_t make_rsrc(uintptr_t base, uint32_t bytes) {
 }
 
 struct FastDec {
-  uintptr_t dst;
   lds_u8 *ring;      // kRing bytes of the newest output
   rsrc_t rin;        // compressed block [0, csize)
   rsrc_t rout;       // block output [0, realcap)
-  uint32_t csize, oend, realcap;
-  uint32_t oc;       // output position of the chunk being painted
-  uint32_t dsrc;     // lane l: source of output byte oc+l (kLitTag | input pos, or output pos)
-  // the previous chunk, fetched but not yet written: its HBM loads stay in
-  // flight while the next chunk is painted
+  uint32_t csize;
+  // the previous piece, fetched but not yet written: its HBM loads stay in
+  // flight while the next piece's sources are worked out
   uint32_t pn, poc;  // live bytes (0: none) and output position
   uint32_t plb, pfb, prb;
 };
 
-// Write the pending chunk into the history ring and to HBM.  Each lane's byte
+// Write the pending piece into the history ring and to HBM.  Each lane's byte
 // arrived in exactly one of its three sources (parked loads read 0).
 __device__ __forceinline__ void fast_retire(FastDec &d, int lane) {
   if (!d.pn) return;
@@ -72,54 +73,37 @@ __device__ __forceinline__ void fast_retire(FastDec &d, int lane) {
   d.pn = 0;
 }
 
-// Resolve and fetch output bytes [oc, oc+nvalid) of the painted chunk; they
-// are written by the next retire, so the loads overlap the next painting.
-__device__ __forceinline__ void fast_flush(FastDec &d, uint32_t nvalid, int lane) {
-  fast_retire(d, lane);  // the ring must hold everything before oc
-  uint32_t src = d.dsrc;
+// Fetch output bytes [pc, pc+nvalid): lane l's byte comes from `src` (kLitTag | input
+// position, or an output position below its own).  They are written by the next retire.
+__device__ __forceinline__ void fast_flush(FastDec &d, uint32_t src, uint32_t pc, uint32_t nvalid,
+                                           int lane) {
+  fast_retire(d, lane);  // the ring must hold everything before pc
   const bool live = uint32_t(lane) < nvalid;
-  // match sources inside this chunk: pointer jumping, each step halves the
-  // remaining hops (sources always point to lower lanes)
+  // match sources inside this piece: pointer jumping, each step halves the
+  // remaining hops (sources always point to lower lanes).  The shuffle is
+  // unconditional: under a lane predicate its source lanes would read zeros.
   for (;;) {
-    const bool intra = live && !(src & kLitTag) && src >= d.oc;
+    const bool intra = live && !(src & kLitTag) && src >= pc;
     if (!ballot(intra)) break;
-    const uint32_t v = uint32_t(__shfl(int(src), intra ? int(src - d.oc) : lane));
-    if (intra) src = v;
+    const uint32_t v = uint32_t(__shfl(int(src), int((src - pc) & 63u)));
+    src = intra ? v : src;
   }
   const bool lit = (src & kLitTag) != 0u;
   const uint32_t q = src & ~kLitTag;
-  const bool ring_ok = !lit && q + kRing >= d.oc;  // still in the history ring
+  const bool ring_ok = !lit && q + kRing >= pc;  // still in the history ring
   const bool far = live && !lit && !ring_ok;
-  // far history was stored >= kRing/64 chunks (>= 64 vector-memory ops) ago:
+  // far history was stored >= kRing/64 pieces (>= 64 vector-memory ops) ago:
   // with in-order vmcnt retirement it has completed, so no wait is needed
   d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live && lit) ? q : kNoAccess, 0, 0);
   d.pfb = __builtin_amdgcn_raw_buffer_load_b8(d.rout, far ? q : kNoAccess, 0, 0);
   asm volatile("" ::: "memory");  // ring bytes stored by other lanes
   d.prb = d.ring[q & kRingMask] & (ring_ok ? 0xFFu : 0u);
   d.pn = nvalid;
-  d.poc = d.oc;
-}
-
-// output [a, b) takes its bytes from source positions s, s+1, ... (tag marks
-// input positions); completes and flushes chunks on the way
-__device__ __forceinline__ void fast_paint(FastDec &d, uint32_t a, uint32_t b, uint32_t s,
-                                           uint32_t tag, int lane) {
-  while (a < b) {
-    const uint32_t ce = d.oc + 64u;
-    const uint32_t e = b < ce ? b : ce;
-    const uint32_t rel = uint32_t(lane) + d.oc - a;
-    if (rel < e - a) d.dsrc = (s + rel) | tag;
-    s += e - a;
-    a = e;
-    if (a == ce) {
-      fast_flush(d, 64u, lane);
-      d.oc = ce;
-    }
-  }
+  d.poc = pc;
 }
 
 // Candidate sequence of lane `lane` of segment [seg, seg+64): the sequence
-// that would start at p = seg+lane, parsed from 24 bytes of registers.
+// that would start at p = seg+lane.
 //   A: next sequence start, kSeqComplex, or kSeqBad
 //   B: literal length | match length << 16 (match length 0: last sequence)
 //   C: offset | (literal start - p) << 16
@@ -127,87 +111,76 @@ struct SegCand {
   uint32_t A, B, C;
 };
 
-// 20 bytes of a lane's window as named words (no array: a runtime-indexed
-// register array would be demoted to scratch)
-struct Win20 {
-  uint32_t w0, w1, w2, w3, w4;
+typedef uint32_t seg_u2 __attribute__((ext_vector_type(2)));
+
+// discovery, first load: the aligned 8 bytes holding the 4 bytes at p
+__device__ __forceinline__ seg_u2 seg_load_head(rsrc_t rin, uint32_t seg, int lane) {
+  return __builtin_amdgcn_raw_buffer_load_b64(rin, (seg + uint32_t(lane)) & ~3u, 0, 0);
+}
+
+// Token and literal length of the candidate at p: ll, header bytes k, flags
+struct SegHead {
+  uint32_t tok, ll, k, lit_end;
+  bool bad, complex;
 };
 
-// 4 bytes starting `k` bytes into the window (k <= 19; bytes past 20 read 0)
-__device__ __forceinline__ uint32_t win4(const Win20 &w, uint32_t k) {
-  const uint32_t j = k >> 2;
-  const uint32_t lo = j == 0 ? w.w0 : j == 1 ? w.w1 : j == 2 ? w.w2 : j == 3 ? w.w3 : w.w4;
-  const uint32_t hi = j == 0 ? w.w1 : j == 1 ? w.w2 : j == 2 ? w.w3 : j == 3 ? w.w4 : 0u;
-  return __builtin_amdgcn_alignbyte(hi, lo, k & 3u);
+__device__ __forceinline__ SegHead seg_head(seg_u2 h, uint32_t csize, uint32_t seg, int lane) {
+  const uint32_t p = seg + uint32_t(lane);
+  const uint32_t w0 = __builtin_amdgcn_alignbyte(h.y, h.x, p & 3u);
+  SegHead r;
+  r.tok = w0 & 0xFFu;
+  uint32_t ll = r.tok >> 4;
+  const uint32_t b1 = (w0 >> 8) & 0xFFu, b2 = (w0 >> 16) & 0xFFu, b3 = w0 >> 24;
+  const bool e0 = ll == 15u;          // length bytes follow
+  const bool e1 = e0 && b1 == 255u;
+  const bool e2 = e1 && b2 == 255u;
+  const bool e3 = e2 && b3 == 255u;   // the run continues past the 4 bytes
+  ll += (e0 ? b1 : 0u) + (e1 ? b2 : 0u) + (e2 ? b3 : 0u);
+  r.k = 1u + uint32_t(e0) + uint32_t(e1) + uint32_t(e2);
+  // read_variable_length(iend-15, initial_check): error if ip >= iend-15; a 255 read at
+  // ip >= iend-15 stops the reference's loop early (loop_error, tolerated for literals)
+  // where this parse would go on
+  const uint32_t lim = csize - 15u;
+  r.bad = (e0 && (p + 1u >= lim || csize < 16u)) || (e1 && p + 2u >= lim) ||
+          (e2 && p + 3u >= lim) || (e3 && p + 4u >= lim) || p >= csize;
+  r.complex = e3;
+  r.ll = ll;
+  r.lit_end = p + r.k + ll;
+  return r;
+}
+
+// discovery, second load: the aligned 8 bytes holding the 4 bytes behind the literals
+__device__ __forceinline__ seg_u2 seg_load_tail(rsrc_t rin, const SegHead &hd) {
+  return __builtin_amdgcn_raw_buffer_load_b64(rin, hd.lit_end & ~3u, 0, 0);
+}
+
+__device__ __forceinline__ SegCand seg_finish(const SegHead &hd, seg_u2 g, uint32_t csize) {
+  const uint32_t dw = __builtin_amdgcn_alignbyte(g.y, g.x, hd.lit_end & 3u);
+  const bool last = hd.lit_end == csize;  // literals-only last sequence
+  const uint32_t off = dw & 0xFFFFu;
+  uint32_t ml = hd.tok & 15u;
+  const uint32_t c1 = (dw >> 16) & 0xFFu, c2 = dw >> 24;
+  const bool f0 = ml == 15u;
+  const bool f1 = f0 && c1 == 255u;
+  const bool f2 = f1 && c2 == 255u;  // the run continues past the 4 bytes
+  ml += (f0 ? c1 : 0u) + (f1 ? c2 : 0u) + uint32_t(kLz4MinMatch);
+  // read_variable_length(iend-LASTLITERALS+1): error once ip >= iend-4, for every byte read
+  const uint32_t m0 = hd.lit_end + 2u;
+  const bool mbad = off == 0u ||  // the reference writes garbage for offset 0
+                    (f0 && (m0 + 1u >= csize - 4u || csize < 5u)) || (f1 && m0 + 2u >= csize - 4u);
+  const bool bad = hd.bad || (!last && !hd.complex && mbad);
+  const bool complex = hd.complex || (!last && f2);
+  const uint32_t next = last ? csize : m0 + uint32_t(f0) + uint32_t(f1);
+  SegCand c;
+  c.A = bad ? kSeqBad : (complex ? kSeqComplex : next);
+  c.B = (hd.ll & 0xFFFFu) | ((last ? 0u : ml) << 16);
+  c.C = (last ? 0u : off) | (hd.k << 16);
+  return c;
 }
 
 __device__ __forceinline__ SegCand seg_parse(const FastDec &d, uint32_t seg, int lane) {
-  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-  const uint32_t p = seg + uint32_t(lane);
-  const uint32_t a = p & ~3u, sh = p & 3u;
-  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(d.rin, a, 0, 0);
-  const u2 x = __builtin_amdgcn_raw_buffer_load_b64(d.rin, a + 16u, 0, 0);
-  Win20 w;  // bytes p .. p+19
-  w.w0 = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
-  w.w1 = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
-  w.w2 = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
-  w.w3 = __builtin_amdgcn_alignbyte(x.x, v.w, sh);
-  w.w4 = __builtin_amdgcn_alignbyte(x.y, x.x, sh);
-  const uint32_t csize = d.csize;
-  SegCand c;
-  const uint32_t tok = w.w0 & 0xFFu;
-  uint32_t ll = tok >> 4, k = 1u;
-  bool complex = false, bad = false;
-  if (ll == 15u) {
-    // read_variable_length(iend-15, initial_check): error if ip >= iend-15
-    if (p + 1u >= csize - 15u || csize < 16u) bad = true;
-    uint32_t b;
-    do {
-      b = (win4(w, k) & 0xFFu);
-      // a 255 read at ip >= iend-15 stops the reference's loop early
-      // (loop_error, tolerated for literals) where this parse would go on
-      if (b == 255u && p + k + 1u >= csize - 15u) bad = true;
-      ll += b;
-      ++k;
-    } while (b == 255u && k < 4u);
-    if (b == 255u) complex = true;  // run continues past the window
-  }
-  const uint32_t lit_end = p + k + ll;
-  uint32_t ml = 0, off = 0, next;
-  if (lit_end == csize) {  // literals-only last sequence
-    next = csize;
-  } else {
-    const uint32_t r = lit_end - p;
-    if (r + 3u > 20u) {
-      complex = true;
-      next = 0;
-    } else {
-      const uint32_t dw = win4(w, r);
-      off = dw & 0xFFFFu;
-      if (off == 0u) bad = true;  // the reference writes garbage for it
-      ml = tok & 15u;
-      uint32_t m = r + 2u;
-      if (ml == 15u) {
-        uint32_t b;
-        do {
-          if (m >= 20u) { complex = true; break; }
-          b = win4(w, m) & 0xFFu;
-          // read_variable_length(iend-LASTLITERALS+1): error once ip >= iend-4
-          if (p + m + 1u >= csize - 4u || csize < 5u) bad = true;
-          ml += b;
-          ++m;
-        } while (b == 255u);
-      }
-      ml += uint32_t(kLz4MinMatch);
-      next = p + m;
-    }
-  }
-  c.A = bad ? kSeqBad : (complex ? kSeqComplex : next);
-  c.B = (ll & 0xFFFFu) | (ml << 16);
-  c.C = off | (k << 16);
-  if (p >= csize) c.A = kSeqBad;  // no sequence can start past the input
-  return c;
+  const SegHead hd = seg_head(seg_load_head(d.rin, seg, lane), d.csize, seg, lane);
+  return seg_finish(hd, seg_load_tail(d.rin, hd), d.csize);
 }
 
 // Byte `i` of the compressed block, wave-uniform (slow path only).
@@ -286,72 +259,76 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t &total) {
   return uint32_t(x) - v;
 }
 
-// Decode one independent block, a whole 64-byte input segment at a time.
-// The chain walk only marks which candidate lanes are real sequences (one
-// v_readlane + one s_bitset per sequence); everything else is vector work
-// over the segment's sequences: output offsets by a lane prefix sum, the
-// reference's acceptance checks by ballot, and the output chunks painted
-// lane-per-byte (LDS scatter of sequence starts + max scan).
-// Returns the decoded size or kFastFallback.
+// Decode one independent block, a whole 64-byte input segment at a time (see the file
+// comment).  Returns the decoded size or kFastFallback.
 __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, uint32_t oend,
                                  uint32_t realcap, lds_u8 *ring, lds_u8 *map, int lane) {
   if (csize < 16u || csize > 65536u || oend > 65536u || oend < 64u) return kFastFallback;
   FastDec d;
-  d.dst = dst;
   d.ring = ring;
   d.rin = make_rsrc(src, csize);
   d.rout = make_rsrc(dst, realcap);
   d.csize = csize;
-  d.oend = oend;
-  d.realcap = realcap;
-  d.oc = 0;
-  d.dsrc = 0;
   d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
+  const uint32_t olimit = realcap < 65536u ? realcap : 65536u;
   uint32_t op = 0, ipn = 0;
   // the last non-final sequence decides the end-of-block margins
   uint32_t last_cpy = 0, last_lit_end = 0, last_mend = 0;
   bool have_last = false;
   uint32_t seg = 0;
   SegCand cur = seg_parse(d, 0u, lane);
-  SegCand nxt = seg_parse(d, 64u, lane);
+  // discovery pipeline: the head of segment seg+64 is parsed and its tail gather issued
+  // before this segment is expanded; the head bytes of seg+128 are in flight
+  seg_u2 h2 = seg_load_head(d.rin, 64u, lane);
   for (;;) {
+    const SegHead nhd = seg_head(h2, csize, seg + 64u, lane);
+    const seg_u2 ng = seg_load_tail(d.rin, nhd);
+    h2 = seg_load_head(d.rin, seg + 128u, lane);
     // ---- walk: which candidate lanes are the real sequences of this segment
-    uint64_t M = 0;
-    uint32_t x = ipn - seg;
-    bool done = false;
-    while (x < 64u) {
-      uint32_t a = __builtin_amdgcn_readlane(cur.A, x);
-      if (a == kSeqComplex) {  // header too long for the lane window: parse it scalar
-        const SegCand s = seq_slow(d.rin, csize, seg + x);
-        const bool me = uint32_t(lane) == x;
-        cur.A = me ? s.A : cur.A;
-        cur.B = me ? s.B : cur.B;
-        cur.C = me ? s.C : cur.C;
-        a = s.A;
+    const uint32_t x0 = ipn - seg;
+    uint64_t M;
+    for (;;) {
+      // bad, complex, leaves the segment, or ends the block (nothing may follow csize)
+      const bool stop = cur.A - seg >= 64u || cur.A == csize;
+      uint32_t J = stop ? 64u : cur.A - seg;
+      bool R = uint32_t(lane) == x0;
+      map[lane] = 0;
+#pragma unroll
+      for (int level = 0; level < 5; ++level) {
+        asm volatile("" ::: "memory");
+        if (R && J < 64u) map[J] = 1;
+        asm volatile("" ::: "memory");
+        R = R || map[lane] != 0;
+        const uint32_t jj = uint32_t(__shfl(int(J), int(J & 63u)));
+        J = J < 64u ? jj : 64u;
       }
-      if (a == kSeqBad) return kFastFallback;
-      M |= 1ull << x;
-      if (a == csize) {  // nothing can follow: must be the literals-only last sequence
-        done = true;
-        break;
-      }
-      x = a - seg;
+      asm volatile("" ::: "memory");
+      M = ballot(R);
+      if (ballot(R && cur.A == kSeqBad)) return kFastFallback;
+      const uint64_t cx = ballot(R && cur.A == kSeqComplex);
+      if (!cx) break;
+      // header too long for the lane's bytes: parse it scalar, then walk again
+      const uint32_t xc = uint32_t(__builtin_ctzll(cx));
+      const SegCand sc = seq_slow(d.rin, csize, seg + xc);
+      if (sc.A == kSeqBad) return kFastFallback;
+      const bool me = uint32_t(lane) == xc;
+      cur.A = me ? sc.A : cur.A;
+      cur.B = me ? sc.B : cur.B;
+      cur.C = me ? sc.C : cur.C;
     }
-    const uint32_t xl = x;  // last member (only meaningful when done)
-#ifdef RDK_DEC_DEBUG
-    if (lane == 0 && seg < 512)
-      printf("seg %u ipn %u x %u M %016lx done %d op %u oc %u\n", seg, ipn, x, (unsigned long)M,
-             int(done), op, d.oc);
-#endif
+    const uint32_t xl = uint32_t(63 - __builtin_clzll(M));  // last member (M holds x0)
+    const uint32_t a_last = __builtin_amdgcn_readlane(cur.A, xl);
+    const bool done = a_last == csize;  // nothing can follow: the literals-only last sequence
     // ---- the segment's sequences, one per member lane, in lane order
     const bool mem = (M >> lane) & 1ull;
     const uint32_t ll = cur.B & 0xFFFFu, ml = cur.B >> 16, off = cur.C & 0xFFFFu;
     const uint32_t ls = seg + uint32_t(lane) + (cur.C >> 16);
     uint32_t T;
-    const uint32_t ostart = op + wave_excl_sum(mem ? ll + ml : 0u, T);
+    const uint32_t len = mem ? ll + ml : 0u;
+    const uint32_t ostart = op + wave_excl_sum(len, T);
     const uint32_t cpy = ostart + ll;
     if (ballot(mem && ml != 0u && off > cpy)) return kFastFallback;  // match < lowPrefix
-    if (op + T > realcap) return kFastFallback;  // the exact path reports the size error
+    if (op + T > olimit) return kFastFallback;  // the exact path reports the size error
     const uint64_t nl = ballot(mem && ml != 0u);
     if (nl) {
       const int j = 63 - __builtin_clzll(nl);
@@ -369,59 +346,47 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
                         last_mend > oend - uint32_t(kLz4LastLiterals)))
         return kFastFallback;
     }
-    // ---- paint output [op, op+T) into 64-byte chunks, flushing full ones
+    // ---- output [op, op+T) in pieces of 64 bytes, lane per byte
     const uint32_t op_new = op + T;
-    const uint32_t ffield = ll | (off << 16);
-    for (uint32_t c = d.oc; c < op_new; c += 64u) {
-      const uint32_t lo = op > c ? op : c;
-      const uint32_t hi = op_new < c + 64u ? op_new : c + 64u;
-      // member whose output starts at or before each lane's byte: starts in
-      // this chunk are scattered into the map and max-scanned; lanes before
-      // the chunk's first start take the member running into the chunk
-      // (compiler barriers: other lanes' LDS stores are invisible to the
-      // optimizer, which would otherwise forward map[lane] = 0 to the read)
+    const uint32_t f1 = ll | (off << 16);
+    const uint32_t f2 = (ostart & 0xFFFFu) | (ls << 16);  // a sequence with bytes starts < 65536
+    uint32_t carry = 0;  // member (lane + 1) whose bytes run into the piece
+    for (uint32_t c = op; c < op_new; c += 64u) {
+      // member whose output starts at or before each lane's byte: starts in this piece are
+      // scattered into the map and max-scanned; lanes before the piece's first start take
+      // the member running into the piece (compiler barriers: other lanes' LDS stores are
+      // invisible to the optimizer, which would otherwise forward map[lane] = 0 to the read)
       map[lane] = 0;
       asm volatile("" ::: "memory");
-      if (mem && ostart >= c && ostart < c + 64u && ll + ml != 0u) map[ostart - c] = uint8_t(lane + 1);
+      if (len != 0u && ostart - c < 64u) map[ostart - c] = uint8_t(lane + 1);
       asm volatile("" ::: "memory");
       uint32_t v = wave_incl_max(map[lane]);
-      const uint64_t before = ballot(mem && ostart < c && ll + ml != 0u);
-      const uint32_t carry = before ? uint32_t(64 - __builtin_clzll(before)) : 0u;
       v = v ? v : carry;
-      const int idx = int(v ? v - 1u : 0u);
-      const uint32_t fo = uint32_t(__shfl(int(ostart), idx));
-      const uint32_t ff = uint32_t(__shfl(int(ffield), idx));
-      const uint32_t fl = uint32_t(__shfl(int(ls), idx));
+      carry = __builtin_amdgcn_readlane(v, 63);
+      const int idx = int((v - 1u) & 63u);
+      const uint32_t g1 = uint32_t(__shfl(int(f1), idx));
+      const uint32_t g2 = uint32_t(__shfl(int(f2), idx));
       const uint32_t o = c + uint32_t(lane);
-      const uint32_t rel = o - fo;
-      const uint32_t s = rel < (ff & 0xFFFFu) ? ((fl + rel) | kLitTag) : (o - (ff >> 16));
-      if (o >= lo && o < hi) d.dsrc = s;
-#ifdef RDK_DEC_DEBUG
-      if (seg == 64 && c == 64 && lane >= 10 && lane < 24)
-        printf("L%d mem %d ostart %u ll %u ml %u off %u ls %u | v %u fo %u ff %08x fl %u s %08x\n",
-               lane, int(mem), ostart, ll, ml, off, ls, v, fo, ff, fl, s);
-#endif
-      if (hi == c + 64u) {
-        fast_flush(d, 64u, lane);
-        d.oc = c + 64u;
-      }
+      const uint32_t rel = (o - g2) & 0xFFFFu;
+      const uint32_t s = rel < (g1 & 0xFFFFu) ? (((g2 >> 16) + rel) | kLitTag) : (o - (g1 >> 16));
+      const uint32_t left = op_new - c;
+      fast_flush(d, s, c, left < 64u ? left : 64u, lane);
     }
     op = op_new;
     if (done) {
-      if (op > d.oc) fast_flush(d, op - d.oc, lane);
       fast_retire(d, lane);
       return int(op);
     }
-    ipn = seg + x;
-    // ---- next segment (usually the prefetched one)
+    ipn = a_last;
+    // ---- next segment (usually the one in the discovery pipeline)
     const uint32_t nseg = ipn & ~63u;
     if (nseg >= csize) return kFastFallback;  // ran off the input without a last sequence
     if (nseg == seg + 64u) {
-      cur = nxt;
+      cur = seg_finish(nhd, ng, csize);
     } else {
       cur = seg_parse(d, nseg, lane);
+      h2 = seg_load_head(d.rin, nseg + 64u, lane);
     }
     seg = nseg;
-    nxt = seg_parse(d, seg + 64u, lane);
   }
 }

@@ -484,7 +484,7 @@ lz4f_blocks_kernel(
     const FrameState *__restrict__ fs, BlockDesc *__restrict__ bd,
     const uint32_t *__restrict__ work_count, const uint32_t *__restrict__ work) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kDecWaves][kRing];
-  __shared__ __attribute__((aligned(16))) uint8_t maps[kDecWaves][64];
+  __shared__ __attribute__((aligned(16))) uint8_t maps[kDecWaves][128];
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
   lds_u8 *ring = (lds_u8 *)rings[uni(threadIdx.x >> 6)];
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void lz4f_seq_kernel(
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
     const uint32_t *__restrict__ out_caps, uint32_t n, FrameState *__restrict__ fs) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kDecWaves][kRing];
-  __shared__ __attribute__((aligned(16))) uint8_t maps[kDecWaves][64];
+  __shared__ __attribute__((aligned(16))) uint8_t maps[kDecWaves][128];
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
   lds_u8 *ring = (lds_u8 *)rings[uni(threadIdx.x >> 6)];
@@ -668,8 +668,8 @@ void launch_decode(uint8_t *scratch, const uint8_t *d_in, const uint64_t *d_in_o
   hipLaunchKernelGGL(lz4f_walk_kernel, dim3((n + 63) / 64), dim3(64), 0, s, d_in, d_in_offs,
                      d_in_lens, n, fs, bd, work_count, work);
   // persistent grid: as many workgroups per CU as the LDS rings and the 32 wave slots allow
-  constexpr unsigned kWgPerCu = (160u * 1024u) / (kDecWaves * (kRing + 64u)) < 32u / kDecWaves
-                                    ? (160u * 1024u) / (kDecWaves * (kRing + 64u))
+  constexpr unsigned kWgPerCu = (160u * 1024u) / (kDecWaves * (kRing + 128u)) < 32u / kDecWaves
+                                    ? (160u * 1024u) / (kDecWaves * (kRing + 128u))
                                     : 32u / kDecWaves;
   const uint64_t want = (uint64_t(n) * kMaxDesc + kDecWaves - 1) / kDecWaves;
   const unsigned cap = 256u * kWgPerCu;

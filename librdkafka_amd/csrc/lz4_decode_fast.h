@@ -44,6 +44,8 @@ constexpr uint32_t kSeqBad = 0xFFFFFFFEu;      // the reference would reject it
 constexpr uint32_t kNoAccess = 0x80000000u;    // out-of-range buffer offset (reads 0)
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// lane mask of a predicate, straight from the compare (no 0/1 round trip through a VGPR)
+__device__ __forceinline__ uint64_t fballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ rsrc_t make_rsrc(uintptr_t base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), 0, int(bytes),
                                            0x00020000);
@@ -51,6 +53,7 @@ __device__ __forceinline__ rsrc_t make_rsrc(uintptr_t base, uint32_t bytes) {
 
 struct FastDec {
   lds_u8 *ring;      // kRing bytes of the newest output
+  lds_u8 *map;       // 128 bytes: [0, 64) per-piece scratch, [64, 128) stores of parked lanes
   rsrc_t rin;        // compressed block [0, csize)
   rsrc_t rout;       // block output [0, realcap)
   uint32_t csize;
@@ -62,11 +65,12 @@ struct FastDec {
 
 // Write the pending piece into the history ring and to HBM.  Each lane's byte
 // arrived in exactly one of its three sources (parked loads read 0).
+// No branches: a lane without a byte stores into its parking slot / out of range.
 __device__ __forceinline__ void fast_retire(FastDec &d, int lane) {
-  if (!d.pn) return;
   const bool live = uint32_t(lane) < d.pn;
   const uint32_t v = d.plb | d.pfb | d.prb;
-  if (live) d.ring[(d.poc + uint32_t(lane)) & kRingMask] = uint8_t(v);
+  lds_u8 *slot = live ? d.ring + ((d.poc + uint32_t(lane)) & kRingMask) : d.map + 64 + lane;
+  *slot = uint8_t(v);
   asm volatile("" ::: "memory");
   __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), d.rout, live ? d.poc + uint32_t(lane) : kNoAccess,
                                       0, 0);
@@ -83,18 +87,20 @@ __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t src, uint32_t pc
   // remaining hops (sources always point to lower lanes).  The shuffle is
   // unconditional: under a lane predicate its source lanes would read zeros.
   for (;;) {
-    const bool intra = live && !(src & kLitTag) && src >= pc;
-    if (!ballot(intra)) break;
+    // (a literal source has the tag bit set and compares below as a huge position: the
+    // signed compare keeps it out)
+    const bool intra = live & (int32_t(src) >= int32_t(pc));
+    if (!fballot(intra)) break;
     const uint32_t v = uint32_t(__shfl(int(src), int((src - pc) & 63u)));
     src = intra ? v : src;
   }
-  const bool lit = (src & kLitTag) != 0u;
+  const bool lit = int32_t(src) < 0;
   const uint32_t q = src & ~kLitTag;
-  const bool ring_ok = !lit && q + kRing >= pc;  // still in the history ring
-  const bool far = live && !lit && !ring_ok;
+  const bool ring_ok = !lit & (q + kRing >= pc);  // still in the history ring
+  const bool far = live & !lit & !ring_ok;
   // far history was stored >= kRing/64 pieces (>= 64 vector-memory ops) ago:
   // with in-order vmcnt retirement it has completed, so no wait is needed
-  d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live && lit) ? q : kNoAccess, 0, 0);
+  d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live & lit) ? q : kNoAccess, 0, 0);
   d.pfb = __builtin_amdgcn_raw_buffer_load_b8(d.rout, far ? q : kNoAccess, 0, 0);
   asm volatile("" ::: "memory");  // ring bytes stored by other lanes
   d.prb = d.ring[q & kRingMask] & (ring_ok ? 0xFFu : 0u);
@@ -132,17 +138,17 @@ __device__ __forceinline__ SegHead seg_head(seg_u2 h, uint32_t csize, uint32_t s
   uint32_t ll = r.tok >> 4;
   const uint32_t b1 = (w0 >> 8) & 0xFFu, b2 = (w0 >> 16) & 0xFFu, b3 = w0 >> 24;
   const bool e0 = ll == 15u;          // length bytes follow
-  const bool e1 = e0 && b1 == 255u;
-  const bool e2 = e1 && b2 == 255u;
-  const bool e3 = e2 && b3 == 255u;   // the run continues past the 4 bytes
+  const bool e1 = e0 & (b1 == 255u);
+  const bool e2 = e1 & (b2 == 255u);
+  const bool e3 = e2 & (b3 == 255u);  // the run continues past the 4 bytes
   ll += (e0 ? b1 : 0u) + (e1 ? b2 : 0u) + (e2 ? b3 : 0u);
   r.k = 1u + uint32_t(e0) + uint32_t(e1) + uint32_t(e2);
   // read_variable_length(iend-15, initial_check): error if ip >= iend-15; a 255 read at
   // ip >= iend-15 stops the reference's loop early (loop_error, tolerated for literals)
   // where this parse would go on
   const uint32_t lim = csize - 15u;
-  r.bad = (e0 && (p + 1u >= lim || csize < 16u)) || (e1 && p + 2u >= lim) ||
-          (e2 && p + 3u >= lim) || (e3 && p + 4u >= lim) || p >= csize;
+  r.bad = (e0 & ((p + 1u >= lim) | (csize < 16u))) | (e1 & (p + 2u >= lim)) |
+          (e2 & (p + 3u >= lim)) | (e3 & (p + 4u >= lim)) | (p >= csize);
   r.complex = e3;
   r.ll = ll;
   r.lit_end = p + r.k + ll;
@@ -161,15 +167,15 @@ __device__ __forceinline__ SegCand seg_finish(const SegHead &hd, seg_u2 g, uint3
   uint32_t ml = hd.tok & 15u;
   const uint32_t c1 = (dw >> 16) & 0xFFu, c2 = dw >> 24;
   const bool f0 = ml == 15u;
-  const bool f1 = f0 && c1 == 255u;
-  const bool f2 = f1 && c2 == 255u;  // the run continues past the 4 bytes
+  const bool f1 = f0 & (c1 == 255u);
+  const bool f2 = f1 & (c2 == 255u);  // the run continues past the 4 bytes
   ml += (f0 ? c1 : 0u) + (f1 ? c2 : 0u) + uint32_t(kLz4MinMatch);
   // read_variable_length(iend-LASTLITERALS+1): error once ip >= iend-4, for every byte read
   const uint32_t m0 = hd.lit_end + 2u;
-  const bool mbad = off == 0u ||  // the reference writes garbage for offset 0
-                    (f0 && (m0 + 1u >= csize - 4u || csize < 5u)) || (f1 && m0 + 2u >= csize - 4u);
-  const bool bad = hd.bad || (!last && !hd.complex && mbad);
-  const bool complex = hd.complex || (!last && f2);
+  const bool mbad = (off == 0u) |  // the reference writes garbage for offset 0
+                    (f0 & ((m0 + 1u >= csize - 4u) | (csize < 5u))) | (f1 & (m0 + 2u >= csize - 4u));
+  const bool bad = hd.bad | (!last & !hd.complex & mbad);
+  const bool complex = hd.complex | (!last & f2);
   const uint32_t next = last ? csize : m0 + uint32_t(f0) + uint32_t(f1);
   SegCand c;
   c.A = bad ? kSeqBad : (complex ? kSeqComplex : next);
@@ -266,6 +272,7 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
   if (csize < 16u || csize > 65536u || oend > 65536u || oend < 64u) return kFastFallback;
   FastDec d;
   d.ring = ring;
+  d.map = map;
   d.rin = make_rsrc(src, csize);
   d.rout = make_rsrc(dst, realcap);
   d.csize = csize;
@@ -289,23 +296,23 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
     uint64_t M;
     for (;;) {
       // bad, complex, leaves the segment, or ends the block (nothing may follow csize)
-      const bool stop = cur.A - seg >= 64u || cur.A == csize;
+      const bool stop = (cur.A - seg >= 64u) | (cur.A == csize);
       uint32_t J = stop ? 64u : cur.A - seg;
       bool R = uint32_t(lane) == x0;
-      map[lane] = 0;
+      // One level: every reached lane marks its successor (a forward permute is a scatter;
+      // lanes that mark nothing send a zero to the entry lane, which nothing else targets
+      // and which is reached anyway), then the successor map is squared.
 #pragma unroll
       for (int level = 0; level < 5; ++level) {
-        asm volatile("" ::: "memory");
-        if (R && J < 64u) map[J] = 1;
-        asm volatile("" ::: "memory");
-        R = R || map[lane] != 0;
+        const bool send = R & (J < 64u);
+        const int t = __builtin_amdgcn_ds_permute(int((send ? J : x0) << 2), int(send));
+        R = R | (t != 0);
         const uint32_t jj = uint32_t(__shfl(int(J), int(J & 63u)));
         J = J < 64u ? jj : 64u;
       }
-      asm volatile("" ::: "memory");
-      M = ballot(R);
-      if (ballot(R && cur.A == kSeqBad)) return kFastFallback;
-      const uint64_t cx = ballot(R && cur.A == kSeqComplex);
+      M = fballot(R);
+      if (fballot(R & (cur.A == kSeqBad))) return kFastFallback;
+      const uint64_t cx = fballot(R & (cur.A == kSeqComplex));
       if (!cx) break;
       // header too long for the lane's bytes: parse it scalar, then walk again
       const uint32_t xc = uint32_t(__builtin_ctzll(cx));
@@ -317,7 +324,7 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
       cur.C = me ? sc.C : cur.C;
     }
     const uint32_t xl = uint32_t(63 - __builtin_clzll(M));  // last member (M holds x0)
-    const uint32_t a_last = __builtin_amdgcn_readlane(cur.A, xl);
+    const uint32_t a_last = uni(__builtin_amdgcn_readlane(cur.A, xl));
     const bool done = a_last == csize;  // nothing can follow: the literals-only last sequence
     // ---- the segment's sequences, one per member lane, in lane order
     const bool mem = (M >> lane) & 1ull;
@@ -327,9 +334,10 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
     const uint32_t len = mem ? ll + ml : 0u;
     const uint32_t ostart = op + wave_excl_sum(len, T);
     const uint32_t cpy = ostart + ll;
-    if (ballot(mem && ml != 0u && off > cpy)) return kFastFallback;  // match < lowPrefix
+    const bool mm = mem & (ml != 0u);
+    if (fballot(mm & (off > cpy))) return kFastFallback;  // match < lowPrefix
     if (op + T > olimit) return kFastFallback;  // the exact path reports the size error
-    const uint64_t nl = ballot(mem && ml != 0u);
+    const uint64_t nl = fballot(mm);
     if (nl) {
       const int j = 63 - __builtin_clzll(nl);
       last_cpy = __builtin_amdgcn_readlane(cpy, j);
@@ -347,18 +355,19 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
         return kFastFallback;
     }
     // ---- output [op, op+T) in pieces of 64 bytes, lane per byte
-    const uint32_t op_new = op + T;
+    const uint32_t op_new = uni(op + T);
     const uint32_t f1 = ll | (off << 16);
     const uint32_t f2 = (ostart & 0xFFFFu) | (ls << 16);  // a sequence with bytes starts < 65536
     uint32_t carry = 0;  // member (lane + 1) whose bytes run into the piece
-    for (uint32_t c = op; c < op_new; c += 64u) {
+    for (uint32_t c = op; c < op_new; c = uni(c + 64u)) {
       // member whose output starts at or before each lane's byte: starts in this piece are
       // scattered into the map and max-scanned; lanes before the piece's first start take
       // the member running into the piece (compiler barriers: other lanes' LDS stores are
       // invisible to the optimizer, which would otherwise forward map[lane] = 0 to the read)
       map[lane] = 0;
       asm volatile("" ::: "memory");
-      if (len != 0u && ostart - c < 64u) map[ostart - c] = uint8_t(lane + 1);
+      const uint32_t rel0 = ostart - c;
+      map[((len != 0u) & (rel0 < 64u)) ? rel0 : 64u + uint32_t(lane)] = uint8_t(lane + 1);
       asm volatile("" ::: "memory");
       uint32_t v = wave_incl_max(map[lane]);
       v = v ? v : carry;
@@ -368,7 +377,9 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
       const uint32_t g2 = uint32_t(__shfl(int(f2), idx));
       const uint32_t o = c + uint32_t(lane);
       const uint32_t rel = (o - g2) & 0xFFFFu;
-      const uint32_t s = rel < (g1 & 0xFFFFu) ? (((g2 >> 16) + rel) | kLitTag) : (o - (g1 >> 16));
+      const uint32_t s_lit = ((g2 >> 16) + rel) | kLitTag, s_mat = o - (g1 >> 16);
+      const uint32_t pick = 0u - uint32_t(rel < (g1 & 0xFFFFu));  // all ones: a literal byte
+      const uint32_t s = (s_lit & pick) | (s_mat & ~pick);
       const uint32_t left = op_new - c;
       fast_flush(d, s, c, left < 64u ? left : 64u, lane);
     }

@@ -422,7 +422,6 @@ static int fixup_framing(uint8_t *in, size_t inlen) {
 int or_rdk_lz4_compress(int proper_hc, int comp_level, const uint8_t *src,
                         size_t len, uint8_t **out, size_t *outlen) {
     *out = NULL;
-    if (comp_level >= 10) return OR_ERR__BAD_COMPRESSION; /* LZ4HC optimal: not restated */
     size_t cap = or_lz4f_compress_bound(len);
     uint8_t *o = (uint8_t *)malloc(cap);
     if (!o) return OR_ERR__CRIT_SYS_RESOURCE;

@@ -1,6 +1,7 @@
 /*
- * lz4hc_oracle.c -- CPU restatement of the LZ4HC hash-chain compressor that
- * librdkafka v1.3.0 reaches for `compression.level` 3..9 (vendored lz4 1.9.2).
+ * lz4hc_oracle.c -- CPU restatement of the LZ4HC compressors that librdkafka
+ * v1.3.0 reaches for `compression.level` 3..12 (vendored lz4 1.9.2): the
+ * hash-chain parser (3..9) and the optimal parser (10..12).
  * TEST INFRASTRUCTURE ONLY (see oracle.h).
  *
  * Path: rd_kafka_lz4_compress (rdkafka_lz4.c:329) -> LZ4F_compressUpdate ->
@@ -8,7 +9,9 @@
  * LZ4F_compressBlockHC (lz4frame.c:782) -> LZ4_compress_HC_extStateHC_fastReset
  * (lz4hc.c:896, limitedOutput) -> LZ4HC_compress_generic_internal (lz4hc.c:758)
  * -> LZ4HC_compress_hashChain (lz4hc.c:532-746) with nbSearches from clTable
- * (lz4hc.c:775-789).  Levels 10..12 (LZ4HC_compress_optimal) are not restated.
+ * (lz4hc.c:775-789), or LZ4HC_compress_optimal (lz4hc.c:1278-1538) for the
+ * lz4opt rows of that table (10: 96 searches, sufficient length 64; 11: 512,
+ * 128; 12: 16384, LZ4_OPT_NUM, full update), favorCompressionRatio.
  *
  * Positions are block-relative.  Every LZ4F block starts a fresh window: the
  * reference shifts `base` by 64 KB per block (LZ4HC_init_internal,
@@ -16,8 +19,9 @@
  * chain delta of 65535 exactly as an empty table would.  "No entry" is
  * therefore -65536 here and no table survives between blocks.  With
  * dictLimit == lowLimit == block start the extDict / dictCtx branches of
- * LZ4HC_InsertAndGetWiderMatch (lz4hc.c:294-310, :412-439) are unreachable,
- * and chainSwap is 0 on the hash-chain path (lz4hc.c:456, :580, :625).
+ * LZ4HC_InsertAndGetWiderMatch (lz4hc.c:294-310, :412-439) are unreachable.
+ * chainSwap is 0 on the hash-chain path (lz4hc.c:456, :580, :625) and 1, with
+ * pattern analysis, under the optimal parser (LZ4HC_FindLongerMatch, :1267).
  *
  * Pinned byte-for-byte against the reference's lz4hc.c compiled by
  * oracle/Makefile into oracle/_ref/ (tests/test_oracle_hc.py) and against the
@@ -35,6 +39,8 @@
 #define HC_NONE (-65536)              /* an index below every window */
 #define HC_MAXDIST 65535              /* LZ4_DISTANCE_MAX */
 #define HC_OPTIMAL_ML 18              /* (ML_MASK-1)+MINMATCH, lz4hc.c:74 */
+#define HC_OPT_NUM (1 << 12)          /* LZ4_OPT_NUM, lz4hc.c:75 */
+#define HC_TRAILING 3                 /* TRAILING_LITERALS, lz4hc.c:1290 */
 
 typedef struct {
     const uint8_t *s;                 /* block start (== lowPrefixPtr) */
@@ -90,19 +96,21 @@ static int hc_rcount_pattern(const uint8_t *s, int p, int low, uint32_t pat) {
     return p0 - p;
 }
 
-/* LZ4HC_InsertAndGetWiderMatch (lz4hc.c:234-442), prefix-only, chainSwap 0,
+/* LZ4HC_InsertAndGetWiderMatch (lz4hc.c:234-442), prefix-only,
  * favorCompressionRatio.  Returns the new longest; *mpos / *spos are updated
  * only on improvement. */
 static int hc_wider(hc_state *st, int ip, int ilow, int ihigh, int longest,
-                    int *mpos, int *spos, int attempts, int pa) {
+                    int *mpos, int *spos, int attempts, int pa, int swap) {
     const uint8_t *s = st->s;
     const int back_room = ip - ilow;
     const uint32_t pat = ld32(s + ip);
     int repeat = 0;                   /* 0 untested, 1 not, 2 confirmed */
     int src_pat_len = 0;
+    int chain_pos = 0;                /* matchChainPos */
     hc_insert(st, ip);
     int m = st->head[hc_hash(pat)];
     while (m >= 0 && attempts) {
+        int len = 0;
         attempts--;
         if (ld16(s + ilow + longest - 1) == ld16(s + m - back_room + longest - 1) &&
             ld32(s + m) == pat) {
@@ -111,11 +119,28 @@ static int hc_wider(hc_state *st, int ip, int ilow, int ihigh, int longest,
                 int lim = (ilow - ip) > (0 - m) ? (ilow - ip) : (0 - m);
                 while (back > lim && s[ip + back - 1] == s[m + back - 1]) back--;
             }
-            int len = HC_MINMATCH + hc_count(s, ip + HC_MINMATCH, m + HC_MINMATCH, ihigh) - back;
+            len = HC_MINMATCH + hc_count(s, ip + HC_MINMATCH, m + HC_MINMATCH, ihigh) - back;
             if (len > longest) { longest = len; *mpos = m + back; *spos = ip + back; }
         }
+        if (swap && len == longest && m + longest <= ip) {
+            /* chain swap (lz4hc.c:312-334): follow the chain of the position inside
+             * the match whose previous occurrence lies furthest back */
+            int dist = 1, step = 1, accel = 1 << 4;
+            const int end = longest - HC_MINMATCH + 1;
+            for (int pos = 0; pos < end; pos += step) {
+                int cd = st->delta[(m + pos) & 0xffff];
+                step = accel++ >> 4;
+                if (cd > dist) { dist = cd; chain_pos = pos; accel = 1 << 4; }
+            }
+            if (dist > 1) {
+                /* `distanceToNextMatch > matchIndex` (lz4hc.c:331) compares with an
+                 * index that starts at 64 KB: never true for a 16-bit delta */
+                m -= dist;
+                continue;
+            }
+        }
         int dnext = st->delta[m & 0xffff];
-        if (pa && dnext == 1) {       /* pattern analysis (lz4hc.c:336-405) */
+        if (pa && dnext == 1 && chain_pos == 0) {   /* pattern analysis (lz4hc.c:336-405) */
             int cand = m - 1;
             if (repeat == 0) {
                 if (((pat & 0xFFFF) == (pat >> 16)) & ((pat & 0xFF) == (pat >> 24))) {
@@ -146,7 +171,7 @@ static int hc_wider(hc_state *st, int ip, int ilow, int ihigh, int longest,
                 continue;
             }
         }
-        m -= dnext;
+        m -= st->delta[(m + chain_pos) & 0xffff];
     }
     return longest;
 }
@@ -189,14 +214,162 @@ static int hc_encode(const uint8_t *s, uint8_t *d, int *op, int oend, int *ip, i
     return 0;
 }
 
-int or_lz4hc_attempts(int level) {   /* clTable, lz4hc.c:775-789 (hash-chain rows) */
+int or_lz4hc_attempts(int level) {   /* clTable, lz4hc.c:775-789 */
     if (level < 1) level = 9;
     if (level < 3) return 2;
+    if (level >= 12) return 16384;
+    if (level == 11) return 512;
+    if (level == 10) return 96;
     return 1 << (level - 1);          /* 3 -> 4 ... 9 -> 256 */
 }
 
+/* LZ4HC_literalsPrice / LZ4HC_sequencePrice (lz4hc.c:1224-1247), in bytes */
+static int hc_lit_price(int litlen) {
+    int price = litlen;
+    if (litlen >= 15) price += 1 + (litlen - 15) / 255;
+    return price;
+}
+static int hc_seq_price(int litlen, int mlen) {
+    int price = 1 + 2 + hc_lit_price(litlen);
+    if (mlen >= 15 + HC_MINMATCH) price += 1 + (mlen - (15 + HC_MINMATCH)) / 255;
+    return price;
+}
+
+typedef struct { int price, off, mlen, litlen; } hc_opt;   /* LZ4HC_optimal_t */
+
+/* LZ4HC_FindLongerMatch (lz4hc.c:1255-1275): forward only, pattern analysis and
+ * chain swap on.  Returns the length (0: none longer than min_len), *off set. */
+static int hc_longer(hc_state *st, int ip, int ihigh, int min_len, int attempts, int *off) {
+    int mpos = 0, spos = ip;
+    int len = hc_wider(st, ip, ip, ihigh, min_len, &mpos, &spos, attempts, 1, 1);
+    if (len <= min_len) return 0;
+    *off = ip - mpos;
+    return len;
+}
+
+/* LZ4HC_compress_optimal (lz4hc.c:1278-1538), limitedOutput */
+static int hc_optimal(hc_state *st, const uint8_t *src, int n, uint8_t *dst, int dst_cap,
+                      int attempts, int sufficient, int full) {
+    hc_opt *opt = (hc_opt *)malloc(sizeof(hc_opt) * (HC_OPT_NUM + HC_TRAILING));
+    if (!opt) return -1;
+    const int mflimit = n - HC_MFLIMIT, matchlimit = n - HC_LASTLITERALS;
+    int ip = 0, anchor = 0, op = 0;
+    if (sufficient >= HC_OPT_NUM) sufficient = HC_OPT_NUM - 1;
+    while (ip <= mflimit) {
+        const int llen = ip - anchor;
+        int best_mlen, best_off, cur, last_pos = 0, foff = 0;
+        const int flen = hc_longer(st, ip, matchlimit, HC_MINMATCH - 1, attempts, &foff);
+        if (flen == 0) { ip++; continue; }
+        if (flen > sufficient) {       /* good enough: immediate encoding (:1318-1326) */
+            if (hc_encode(src, dst, &op, dst_cap, &ip, &anchor, flen, ip - foff)) goto overflow;
+            continue;
+        }
+        for (int r = 0; r < HC_MINMATCH; r++) {            /* :1329-1338 */
+            opt[r].mlen = 1; opt[r].off = 0; opt[r].litlen = llen + r;
+            opt[r].price = hc_lit_price(llen + r);
+        }
+        for (int ml = HC_MINMATCH; ml <= flen; ml++) {     /* :1340-1352 */
+            opt[ml].mlen = ml; opt[ml].off = foff; opt[ml].litlen = llen;
+            opt[ml].price = hc_seq_price(llen, ml);
+        }
+        last_pos = flen;
+        for (int a = 1; a <= HC_TRAILING; a++) {           /* :1354-1362 */
+            opt[last_pos + a].mlen = 1; opt[last_pos + a].off = 0; opt[last_pos + a].litlen = a;
+            opt[last_pos + a].price = opt[last_pos].price + hc_lit_price(a);
+        }
+        for (cur = 1; cur < last_pos; cur++) {             /* :1365-1459 */
+            const int cp = ip + cur;
+            int noff = 0, nlen;
+            if (cp > mflimit) break;
+            if (full) {
+                if (opt[cur + 1].price <= opt[cur].price &&
+                    opt[cur + HC_MINMATCH].price < opt[cur].price + 3) continue;
+            } else {
+                if (opt[cur + 1].price <= opt[cur].price) continue;
+            }
+            if (full) nlen = hc_longer(st, cp, matchlimit, HC_MINMATCH - 1, attempts, &noff);
+            else nlen = hc_longer(st, cp, matchlimit, last_pos - cur, attempts, &noff);
+            if (!nlen) continue;
+            if (nlen > sufficient || nlen + cur >= HC_OPT_NUM) {   /* :1391-1398 */
+                best_mlen = nlen; best_off = noff; last_pos = cur + 1;
+                goto encode;
+            }
+            {   const int base_ll = opt[cur].litlen;               /* :1401-1413 */
+                for (int ll = 1; ll < HC_MINMATCH; ll++) {
+                    const int price = opt[cur].price - hc_lit_price(base_ll) + hc_lit_price(base_ll + ll);
+                    const int pos = cur + ll;
+                    if (price < opt[pos].price) {
+                        opt[pos].mlen = 1; opt[pos].off = 0; opt[pos].litlen = base_ll + ll;
+                        opt[pos].price = price;
+                    }
+                }
+            }
+            for (int ml = HC_MINMATCH; ml <= nlen; ml++) {         /* :1416-1449 */
+                const int pos = cur + ml;
+                int price, ll;
+                if (opt[cur].mlen == 1) {
+                    ll = opt[cur].litlen;
+                    price = (cur > ll ? opt[cur - ll].price : 0) + hc_seq_price(ll, ml);
+                } else {
+                    ll = 0;
+                    price = opt[cur].price + hc_seq_price(0, ml);
+                }
+                if (pos > last_pos + HC_TRAILING || price <= opt[pos].price) {
+                    if (ml == nlen && last_pos < pos) last_pos = pos;
+                    opt[pos].mlen = ml; opt[pos].off = noff; opt[pos].litlen = ll;
+                    opt[pos].price = price;
+                }
+            }
+            for (int a = 1; a <= HC_TRAILING; a++) {               /* :1451-1458 */
+                opt[last_pos + a].mlen = 1; opt[last_pos + a].off = 0; opt[last_pos + a].litlen = a;
+                opt[last_pos + a].price = opt[last_pos].price + hc_lit_price(a);
+            }
+        }
+        best_mlen = opt[last_pos].mlen;
+        best_off = opt[last_pos].off;
+        cur = last_pos - best_mlen;
+    encode:                                                        /* :1466-1498 */
+        {   int cand = cur, sel_ml = best_mlen, sel_off = best_off;
+            for (;;) {                 /* reverse traversal */
+                const int next_ml = opt[cand].mlen, next_off = opt[cand].off;
+                opt[cand].mlen = sel_ml; opt[cand].off = sel_off;
+                sel_ml = next_ml; sel_off = next_off;
+                if (next_ml > cand) break;
+                cand -= next_ml;
+            }
+        }
+        {   int r = 0;
+            while (r < last_pos) {
+                const int ml = opt[r].mlen, off = opt[r].off;
+                if (ml == 1) { ip++; r++; continue; }
+                r += ml;
+                if (hc_encode(src, dst, &op, dst_cap, &ip, &anchor, ml, ip - off)) goto overflow;
+            }
+        }
+    }
+    {   const int run = n - anchor;   /* :1501-1526 */
+        const int ext = (run + 255 - 15) / 255;
+        if (op + 1 + ext + run > dst_cap) goto overflow;
+        if (run >= 15) {
+            int a = run - 15;
+            dst[op++] = 15 << 4;
+            for (; a >= 255; a -= 255) dst[op++] = 255;
+            dst[op++] = (uint8_t)a;
+        } else {
+            dst[op++] = (uint8_t)(run << 4);
+        }
+        memcpy(dst + op, src + anchor, (size_t)run);
+        op += run;
+    }
+    free(opt);
+    return op;
+overflow:
+    free(opt);
+    return 0;
+}
+
 int or_lz4hc_compress_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap, int level) {
-    if (level >= 10) return -1;       /* LZ4HC_compress_optimal: not restated */
+    if (level > 12) level = 12;       /* MIN(LZ4HC_CLEVEL_MAX, cLevel), lz4hc.c:798 */
     const int attempts = or_lz4hc_attempts(level);
     const int pa = attempts > 128;    /* lz4hc.c:544 */
     hc_state *st = (hc_state *)malloc(sizeof *st);
@@ -204,6 +377,12 @@ int or_lz4hc_compress_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap
     for (int i = 0; i < (1 << HC_HASHLOG); i++) st->head[i] = HC_NONE;
     st->s = src;
     st->next = 0;
+    if (level >= 10) {
+        const int r = hc_optimal(st, src, n, dst, dst_cap, attempts,
+                                 level == 10 ? 64 : level == 11 ? 128 : HC_OPT_NUM, level == 12);
+        free(st);
+        return r;
+    }
 
     const int mflimit = n - HC_MFLIMIT, matchlimit = n - HC_LASTLITERALS;
     int ip = 0, anchor = 0, op = 0, unused = 0;
@@ -212,12 +391,12 @@ int or_lz4hc_compress_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap
     if (n < HC_MFLIMIT + 1) goto last;
     while (ip <= mflimit) {
         /* LZ4HC_InsertAndFindBestMatch (lz4hc.c:445-457) */
-        ml = hc_wider(st, ip, ip, matchlimit, HC_MINMATCH - 1, &ref, &unused, attempts, pa);
+        ml = hc_wider(st, ip, ip, matchlimit, HC_MINMATCH - 1, &ref, &unused, attempts, pa, 0);
         if (ml < HC_MINMATCH) { ip++; continue; }
         start0 = ip; ref0 = ref; ml0 = ml;
     search2:
         if (ip + ml <= mflimit)
-            ml2 = hc_wider(st, ip + ml - 2, ip, matchlimit, ml, &ref2, &start2, attempts, pa);
+            ml2 = hc_wider(st, ip + ml - 2, ip, matchlimit, ml, &ref2, &start2, attempts, pa, 0);
         else
             ml2 = ml;
         if (ml2 == ml) {
@@ -234,7 +413,7 @@ int or_lz4hc_compress_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap
             if (corr > 0) { start2 += corr; ref2 += corr; ml2 -= corr; }
         }
         if (start2 + ml2 <= mflimit)
-            ml3 = hc_wider(st, start2 + ml2 - 3, start2, matchlimit, ml2, &ref3, &start3, attempts, pa);
+            ml3 = hc_wider(st, start2 + ml2 - 3, start2, matchlimit, ml2, &ref3, &start3, attempts, pa, 0);
         else
             ml3 = ml2;
         if (ml3 == ml2) {

@@ -13,8 +13,9 @@ Outputs (all data, no reference source):
                               the reference's rd_kafka_lz4_compress path makes
                               (vendored lz4 1.9.2 LZ4F), and of its payload.
   frame_*.lz4              -- the frames themselves for inputs <= 64 KiB.
-  lz4hc_frames.json        -- the same for compression.level 3..9 (LZ4HC hash
-                              chain, lz4frame.c:782 -> lz4hc.c:532-746).
+  lz4hc_frames.json        -- the same for compression.level 3..12 (LZ4HC hash
+                              chain, lz4frame.c:782 -> lz4hc.c:532-746, and the
+                              optimal parser of levels 10..12, lz4hc.c:1278).
   lz4f_decode_cases.json   -- deterministic malformed / edge-case frames and
                               the reference decoder's verdict (err, len,
                               sha256), exercising rdkafka_lz4.c:167-317.
@@ -108,11 +109,11 @@ HC_INPUTS = ("json_s42_65536", "json_s42_65537", "json_s42_262144", "json_s7_13"
 
 
 def hc_frames() -> None:
-    """LZ4HC (levels 3..9) frames of the reference's rd_kafka_lz4_compress path."""
+    """LZ4HC (levels 3..12) frames of the reference's rd_kafka_lz4_compress path."""
     out = {}
     for name in HC_INPUTS:
         data = input_by_name(name)
-        for level in range(3, 10):
+        for level in range(3, 13):
             err, fr = O.ref_rdk_lz4_compress(data, comp_level=level)
             assert err == 0
             e2, payload, _ = O.ref_rdk_lz4_decompress(fr, max_msg_size=1 << 30)

@@ -1,8 +1,9 @@
-"""LZ4HC (compression.level 3..9) restatement (oracle/lz4hc_oracle.c) pinned
+"""LZ4HC (compression.level 3..12) restatement (oracle/lz4hc_oracle.c) pinned
 against frames made by the reference's own lz4hc.c build (tests/golden/
 lz4hc_frames.json) and, when oracle/_ref is built, live block-level
 differential tests against LZ4_compress_HC_extStateHC_fastReset
-(lz4hc.c:896) -- including the level-9 pattern analysis (lz4hc.c:336-405)."""
+(lz4hc.c:896) -- including the level-9 pattern analysis (lz4hc.c:336-405) and
+the optimal parser with its chain swap (levels 10..12, lz4hc.c:1278, :312-334)."""
 import hashlib
 import importlib.util
 import os
@@ -28,7 +29,7 @@ def _mg():
 def test_lz4hc_frames_match_reference_golden(oracle_mod, golden):
     mg = _mg()
     recs = golden("lz4hc_frames.json")
-    assert len(recs) == len(mg.HC_INPUTS) * 7
+    assert len(recs) == len(mg.HC_INPUTS) * 10
     for key, rec in recs.items():
         data = mg.input_by_name(rec["input"])
         err, fr = oracle_mod.rdk_lz4_compress(data, comp_level=rec["level"])
@@ -51,7 +52,7 @@ def _hc_cases():
     return cases
 
 
-@pytest.mark.parametrize("level", range(3, 10))
+@pytest.mark.parametrize("level", range(3, 13))
 def test_lz4hc_block_differential_vs_reference(oracle_mod, level):
     if not oracle_mod.ref_available():
         pytest.skip("oracle/_ref not built (no /root/reference)")
@@ -60,6 +61,7 @@ def test_lz4hc_block_differential_vs_reference(oracle_mod, level):
             oracle_mod.ref_lz4hc_compress_block(d, level), (level, i, len(d))
 
 
-def test_lz4hc_levels_above_9_not_restated(oracle_mod):
-    err, _ = oracle_mod.rdk_lz4_compress(b"x" * 1000, comp_level=10)
-    assert err == -198
+def test_lz4hc_levels_above_12_clamp(oracle_mod):
+    """MIN(LZ4HC_CLEVEL_MAX, cLevel), lz4hc.c:798"""
+    d = W.gen_json(20000, 3)
+    assert oracle_mod.lz4hc_compress_block(d, 13) == oracle_mod.lz4hc_compress_block(d, 12)

@@ -1115,12 +1115,10 @@ RDK_API int rdk_hip_lz4f_compress(const void *d_in, const uint64_t *d_in_offs,
   Ctx *c = ctx();
   if (!c) return RDK_HIP_E_NODEV;
   if (!n) return RDK_HIP_OK;
-  if (level >= 10)
-    return set_error(RDK_HIP_E_INVAL, "LZ4HC optimal levels (>=10) are not implemented");
   if (!d_in || !d_in_offs || !d_in_lens || !d_out || !d_out_offs || !d_out_lens)
     return set_error(RDK_HIP_E_INVAL, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (level >= 3)  // LZ4F_selectCompression (lz4frame.c:797-805): LZ4HC hash chain
+  if (level >= 3)  // LZ4F_selectCompression (lz4frame.c:797-805): LZ4HC (hash chain 3..9, optimal 10+)
     return lz4hc_compress_device(static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
                                  static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n, level, s);
   const int accel = level < 0 ? -level + 1 : 1;  // LZ4F_compressBlock, lz4frame.c:766

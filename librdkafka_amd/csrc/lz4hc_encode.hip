@@ -1,5 +1,5 @@
-// lz4hc_encode.hip -- LZ4F frame compression at compression.level 3..9 (LZ4HC
-// hash chain) on gfx950.
+// lz4hc_encode.hip -- LZ4F frame compression at compression.level 3..12 (LZ4HC:
+// the hash-chain parser of levels 3..9 and the optimal parser of 10..12) on gfx950.
 //
 // Replaces rd_kafka_lz4_compress (rdkafka_lz4.c:329) -> LZ4F_makeBlock
 // (lz4frame.c:739, dstCapacity = srcSize-1) -> LZ4F_compressBlockHC
@@ -31,6 +31,17 @@
 //      a block that does not fit in srcSize-1 bytes is stored raw (bit 31).
 // Block k of frame f goes to the same worst-case slot as the level-0 engine;
 // lz4f_assemble_kernel (lz4_encode.hip) then builds the frame.
+//
+// Levels 10..12 (LZ4HC_compress_optimal, lz4hc.c:1278-1538; clTable rows
+// lz4hc.c:786-788) share the build and the encoder.  Their search
+// (LZ4HC_FindLongerMatch, lz4hc.c:1255) looks forward only, with pattern analysis
+// and the chain swap (lz4hc.c:312-334): after a candidate that ties or beats the
+// longest match, the walk moves to the chain of the position inside that match
+// whose previous occurrence lies furthest back.  hc_search_swap() evaluates 64
+// candidates of the current chain at once and replays them in order; a swap
+// restarts it on the new chain (the sorted position list serves any position's
+// chain, not only ip's).  The price table of the dynamic program lives in the
+// wave's HBM scratch; its per-length loops run one length per lane.
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -46,7 +57,11 @@ constexpr int kHcHashLog = 15;               // lz4hc.h:196
 constexpr uint32_t kHcNone = 0xFFFFFFFFu;
 constexpr int kHcOptimalML = 18;             // lz4hc.c:74
 constexpr size_t kHcTab = size_t(4) << kHcHashLog;  // head / bucket start, u32
-constexpr size_t kHcScratch = kHcTab + 3 * 65536 * 2 + 65536 * 4;  // + chain, rank, sorted (u16), tr (u32)
+constexpr int kHcOptNum = 1 << 12;           // LZ4_OPT_NUM, lz4hc.c:75
+constexpr int kHcTrailing = 3;               // TRAILING_LITERALS, lz4hc.c:1290
+constexpr size_t kHcOptBytes = size_t(kHcOptNum + 64) * 16;  // price table of the optimal parser
+// + chain, rank, sorted (u16), tr (u32), opt (16 B entries)
+constexpr size_t kHcScratch = kHcTab + 3 * 65536 * 2 + 65536 * 4 + kHcOptBytes;
 constexpr unsigned kHcGrid = 4096;  // 16 waves per CU (the kernel fits 20)
 
 struct HcBlock {
@@ -56,6 +71,7 @@ struct HcBlock {
   uint16_t *rank;    // index of the position inside its hash bucket
   uint16_t *sorted;  // positions ordered by (hash, position)
   uint32_t *tr;      // per position: its index in sorted | its rank << 16
+  int4 *opt;         // LZ4HC_optimal_t[]: x price, y off, z mlen, w litlen (levels 10..12)
   int attempts;      // nbSearches
   int pa;            // patternAnalysis (levels 9+)
   int lane;
@@ -233,17 +249,39 @@ __device__ void hc_build(const HcBlock &b, int npos) {
   __threadfence_block();
 }
 
+// The chain swap's scan (lz4hc.c:315-329) over the chain deltas of the match at m:
+// `dist` = the largest delta met on the accelerating schedule, `cp` = its position
+// (left alone when no delta beats 1).  64 deltas per load, the schedule replayed
+// on them with v_readlane.
+__device__ void hc_swap_scan(const HcBlock &b, int m, int longest, int &dist, int &cp) {
+  const int end = longest - kLz4MinMatch + 1;
+  int step = 1, accel = 1 << 4, pos = 0;
+  dist = 1;
+  for (int base = 0; base < end; base += 64) {
+    const uint32_t cd = base + b.lane < end ? uint32_t(b.chain[m + base + b.lane]) : 0u;
+    const int lim = end < base + 64 ? end : base + 64;
+    while (pos < lim) {
+      const int c = int(__builtin_amdgcn_readlane(cd, pos - base));
+      step = accel++ >> 4;
+      if (c > dist) { dist = c; cp = pos; accel = 1 << 4; }
+      pos += step;
+    }
+  }
+}
+
 // LZ4HC_InsertAndGetWiderMatch one candidate at a time (repetitive patterns
-// at level 9, where pattern analysis may redirect the walk).
+// where pattern analysis may redirect the walk: level 9 and the optimal parser).
 __device__ int hc_search_serial(const HcBlock &b, int ip, int ilow, int ihigh, int longest,
-                                int &mpos, int &spos, uint32_t pat) {
+                                int &mpos, int &spos, uint32_t pat, bool swap) {
   const uintptr_t s = b.s;
   const int br = ip - ilow;
   int attempts = b.attempts;
   int repeat = 0, src_pat_len = 0;  // 0 untested, 1 not, 2 confirmed
+  int cp = 0;                       // matchChainPos
   int m = ip - int(b.chain[ip]);
   while (m >= 0 && attempts) {
     attempts--;
+    int len = 0;
     {
       const int a = ilow + longest - 1, c = m - br + longest - 1;
       if (ldb(s + a) == ldb(s + c) && ldb(s + a + 1) == ldb(s + c + 1) && ld32u(s + m) == pat) {
@@ -252,12 +290,20 @@ __device__ int hc_search_serial(const HcBlock &b, int ip, int ilow, int ihigh, i
           const int lim = (ilow - ip) > -m ? (ilow - ip) : -m;
           while (back > lim && ldb(s + ip + back - 1) == ldb(s + m + back - 1)) back--;
         }
-        const int len = 4 + hc_count(s, ip + 4, m + 4, ihigh) - back;
+        len = 4 + hc_count(s, ip + 4, m + 4, ihigh) - back;
         if (len > longest) { longest = len; mpos = m + back; spos = ip + back; }
       }
     }
+    if (swap && len == longest && m + longest <= ip) {  // lz4hc.c:312-334
+      int dist;
+      hc_swap_scan(b, m, longest, dist, cp);
+      if (dist > 1) {
+        m -= dist;
+        continue;
+      }
+    }
     const int dnext = b.chain[m];
-    if (b.pa && dnext == 1) {
+    if (b.pa && dnext == 1 && cp == 0) {
       const int cand = m - 1;
       if (repeat == 0) {
         if (((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24))) {
@@ -288,7 +334,7 @@ __device__ int hc_search_serial(const HcBlock &b, int ip, int ilow, int ihigh, i
         continue;
       }
     }
-    m -= dnext;
+    m -= int(b.chain[m + cp]);
   }
   return longest;
 }
@@ -300,7 +346,7 @@ __device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int long
   const int lane = b.lane;
   const uint32_t pat = ld32u(s + ip);
   if (b.pa && ((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24)))
-    return hc_search_serial(b, ip, ilow, ihigh, longest, mpos, spos, pat);
+    return hc_search_serial(b, ip, ilow, ihigh, longest, mpos, spos, pat, false);
   const int br = ip - ilow;
   const uint32_t t = b.tr[ip];  // one load instead of rank -> hash -> bucket start
   const int r = int(t >> 16);
@@ -520,11 +566,237 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n) {
   return op;
 }
 
+// ------------------------------------------------------------ levels 10..12
+// LZ4HC_InsertAndGetWiderMatch as LZ4HC_FindLongerMatch drives it (forward only,
+// chain swap on) for a pattern that is not one repeated byte, so that pattern
+// analysis never redirects the walk.  64 candidates of the current chain per step.
+__device__ int hc_search_swap(const HcBlock &b, int ip, int ihigh, int longest, int &mpos,
+                              uint32_t pat) {
+  const uintptr_t s = b.s;
+  const int lane = b.lane;
+  int attempts = b.attempts;
+  int q = ip, cp = 0;  // the walk follows the chain of position q = candidate + cp
+  for (;;) {
+    const uint32_t t = b.tr[q];
+    const int r = int(t >> 16), top = int(t & 0xFFFFu) - 1;
+    const int total = r < attempts ? r : attempts;
+    bool swapped = false;
+    for (int c0 = 0; c0 < total; c0 += 64) {
+      const int j = c0 + lane;
+      const int m = j < total ? int(b.sorted[top - j]) - cp : -1;
+      const bool valid = m >= 0;
+      const bool ok32 = valid && ld32u(s + m) == pat;
+      int len = 0;
+      if (ok32) len = 4 + hc_count(s, ip + 4, m + 4, ihigh);
+      int k0 = 0;
+      for (;;) {  // the reference's order: the next candidate that ties or beats `longest`
+        bool pass = ok32 && lane >= k0 && len >= longest;
+        if (pass && len == longest) {
+          // only a count cut short by ihigh can tie; the read16 prefilter (lz4hc.c:284)
+          // then decides whether the reference measured this candidate at all
+          const int a = ip + longest - 1, c = m + longest - 1;
+          pass = ldb(s + a) == ldb(s + c) && ldb(s + a + 1) == ldb(s + c + 1);
+        }
+        const uint64_t mk = ballot(pass);
+        if (!mk) break;
+        const int k = __builtin_ctzll(mk);
+        const int lk = __shfl(len, k), mm = __shfl(m, k);
+        if (lk > longest) { longest = lk; mpos = mm; }
+        if (mm + longest <= ip) {  // chain swap, lz4hc.c:312-334
+          int dist, ncp = cp;
+          hc_swap_scan(b, mm, longest, dist, ncp);
+          if (dist > 1) {
+            cp = ncp;
+            attempts -= c0 + k + 1;
+            q = mm + cp;
+            swapped = true;
+            break;
+          }
+        }
+        k0 = k + 1;
+      }
+      if (swapped) break;
+      if (ballot(j < total && !valid)) return longest;  // the chain left the block: the walk ends
+    }
+    if (!swapped || attempts <= 0) break;  // chain or attempts used up
+  }
+  return longest;
+}
+
+// LZ4HC_FindLongerMatch (lz4hc.c:1255-1275), favorCompressionRatio: the length
+// (0 when nothing beats min_len) and the offset
+__device__ int hc_longer(const HcBlock &b, int ip, int ihigh, int min_len, int &off) {
+  const uint32_t pat = ld32u(b.s + ip);
+  int mpos = 0, spos = ip, len;
+  if (((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24)))
+    len = hc_search_serial(b, ip, ip, ihigh, min_len, mpos, spos, pat, true);
+  else
+    len = hc_search_swap(b, ip, ihigh, min_len, mpos, pat);
+  if (len <= min_len) return 0;
+  off = ip - mpos;
+  return len;
+}
+
+// LZ4HC_literalsPrice / LZ4HC_sequencePrice (lz4hc.c:1224-1247), in bytes
+__device__ __forceinline__ int hc_lit_price(int litlen) {
+  return litlen + (litlen >= 15 ? 1 + (litlen - 15) / 255 : 0);
+}
+__device__ __forceinline__ int hc_seq_price(int litlen, int mlen) {
+  return 3 + hc_lit_price(litlen) + (mlen >= 19 ? 1 + (mlen - 19) / 255 : 0);
+}
+
+// opt[] accessors: entries are written by one lane (or one entry per lane) and read
+// back by the whole wave; hc_opt_sync() between a write and a dependent read.
+__device__ __forceinline__ int4 hc_opt_ld(const HcBlock &b, int i) { return b.opt[i]; }
+__device__ __forceinline__ void hc_opt_st(const HcBlock &b, int i, int price, int off, int mlen,
+                                          int litlen) {
+  if (b.lane == 0) b.opt[i] = make_int4(price, off, mlen, litlen);
+}
+__device__ __forceinline__ void hc_opt_sync() { __threadfence_block(); }
+
+// opt[last+1 .. last+3]: literals after the last match (lz4hc.c:1354-1362, :1451-1458)
+__device__ __forceinline__ void hc_opt_trailing(const HcBlock &b, int last, int last_price) {
+  if (b.lane >= 1 && b.lane <= kHcTrailing)
+    b.opt[last + b.lane] = make_int4(last_price + hc_lit_price(b.lane), 0, 1, b.lane);
+}
+
+// LZ4HC_compress_optimal (lz4hc.c:1278-1538), limitedOutput.  Returns the compressed
+// size or 0 when the block does not fit in n-1 bytes.  n >= 13.
+__device__ int hc_optimal_block(const HcBlock &b, uintptr_t dst, int n, int sufficient, bool full) {
+  const int mflimit = n - kLz4MFLimit, matchlimit = n - kLz4LastLiterals, oend = n - 1;
+  const int lane = b.lane;
+  hc_build(b, mflimit + 1);
+  if (sufficient >= kHcOptNum) sufficient = kHcOptNum - 1;
+  int ip = 0, anchor = 0, op = 0;
+  while (ip <= mflimit) {
+    const int llen = ip - anchor;
+    int best_mlen, best_off, cur, last_pos, foff = 0;
+    const int flen = hc_longer(b, ip, matchlimit, kLz4MinMatch - 1, foff);
+    if (flen == 0) { ip++; continue; }
+    if (flen > sufficient) {  // good enough: immediate encoding (lz4hc.c:1318-1326)
+      if (hc_encode(b, dst, op, oend, ip, anchor, flen, ip - foff)) return 0;
+      continue;
+    }
+    // prices of the first positions: literals (lz4hc.c:1329-1338), then the first match at
+    // every length (:1340-1352), one entry per lane
+    for (int base = 0; base <= flen; base += 64) {
+      const int r = base + lane;
+      if (r < kLz4MinMatch) b.opt[r] = make_int4(hc_lit_price(llen + r), 0, 1, llen + r);
+      else if (r <= flen) b.opt[r] = make_int4(hc_seq_price(llen, r), foff, r, llen);
+    }
+    last_pos = flen;
+    hc_opt_trailing(b, last_pos, hc_seq_price(llen, flen));
+    hc_opt_sync();
+    bool direct = false;
+    for (cur = 1; cur < last_pos; cur++) {  // lz4hc.c:1365-1459
+      const int cpos = ip + cur;
+      if (cpos > mflimit) break;
+      const int4 oc = hc_opt_ld(b, cur);
+      const int p1 = hc_opt_ld(b, cur + 1).x, p4 = hc_opt_ld(b, cur + kLz4MinMatch).x;
+      // not useful to search here if the next position is as cheap (:1372-1381)
+      if (full ? (p1 <= oc.x && p4 < oc.x + 3) : (p1 <= oc.x)) continue;
+      int noff = 0;
+      const int nlen = hc_longer(b, cpos, matchlimit, full ? kLz4MinMatch - 1 : last_pos - cur, noff);
+      if (!nlen) continue;
+      if (nlen > sufficient || nlen + cur >= kHcOptNum) {  // immediate encoding (:1391-1398)
+        best_mlen = nlen;
+        best_off = noff;
+        last_pos = cur + 1;
+        direct = true;
+        break;
+      }
+      // literals after cur (:1401-1413), one length per lane
+      if (lane >= 1 && lane < kLz4MinMatch) {
+        const int price = oc.x - hc_lit_price(oc.w) + hc_lit_price(oc.w + lane);
+        if (price < b.opt[cur + lane].x) b.opt[cur + lane] = make_int4(price, 0, 1, oc.w + lane);
+      }
+      // the match at cur at every length (:1416-1449), one length per lane
+      int ll, pbase;
+      if (oc.z == 1) {
+        ll = oc.w;
+        pbase = cur > ll ? hc_opt_ld(b, cur - ll).x : 0;
+      } else {
+        ll = 0;
+        pbase = oc.x;
+      }
+      int new_last = last_pos;
+      for (int base = kLz4MinMatch; base <= nlen; base += 64) {
+        const int ml = base + lane;
+        if (ml <= nlen) {
+          const int pos = cur + ml;
+          const int price = pbase + hc_seq_price(ll, ml);
+          if (pos > last_pos + kHcTrailing || price <= b.opt[pos].x) {
+            if (ml == nlen && last_pos < pos) new_last = pos;
+            b.opt[pos] = make_int4(price, noff, ml, ll);
+          }
+        }
+      }
+      // only the lane of the last length can have moved last_pos
+      last_pos = int(__builtin_amdgcn_readlane(new_last, (nlen - kLz4MinMatch) & 63));
+      hc_opt_sync();
+      hc_opt_trailing(b, last_pos, hc_opt_ld(b, last_pos).x);
+      hc_opt_sync();
+    }
+    if (!direct) {
+      const int4 ol = hc_opt_ld(b, last_pos);
+      best_mlen = ol.z;
+      best_off = ol.y;
+      cur = last_pos - best_mlen;
+    }
+    {  // reverse traversal: the cheapest path becomes a forward list (lz4hc.c:1470-1484)
+      int cand = cur, sel_ml = best_mlen, sel_off = best_off;
+      for (;;) {
+        const int4 o = hc_opt_ld(b, cand);
+        hc_opt_st(b, cand, o.x, sel_off, sel_ml, o.w);
+        sel_ml = o.z;
+        sel_off = o.y;
+        if (o.z > cand) break;
+        cand -= o.z;
+      }
+      hc_opt_sync();
+    }
+    {  // encode the recorded sequences in order (lz4hc.c:1487-1498), 64 entries per load
+      int r = 0, rb = -64;
+      int4 e = make_int4(0, 0, 0, 0);
+      while (r < last_pos) {
+        if (r >= rb + 64) {
+          rb = r;
+          e = b.opt[rb + lane];  // entries past last_pos are never used
+        }
+        const int ml = int(__builtin_amdgcn_readlane(e.z, r - rb));
+        if (ml == 1) { ip++; r++; continue; }
+        const int off = int(__builtin_amdgcn_readlane(e.y, r - rb));
+        r += ml;
+        if (hc_encode(b, dst, op, oend, ip, anchor, ml, ip - off)) return 0;
+      }
+    }
+  }
+  {  // last literals (lz4hc.c:1501-1526)
+    const int run = n - anchor;
+    if (op + 1 + (run + 255 - 15) / 255 + run > oend) return 0;
+    if (run >= 15) {
+      const int a = run - 15;
+      if (lane == 0) stb(dst + op, 15u << 4);
+      hc_run(dst + op + 1, a / 255, a % 255, lane);
+      op += 1 + a / 255 + 1;
+    } else {
+      if (lane == 0) stb(dst + op, uint32_t(run) << 4);
+      op += 1;
+    }
+    hc_copy(dst + op, b.s + anchor, run, lane);
+    op += run;
+  }
+  return op;
+}
+
+// OPT: the optimal parser (levels 10..12), a kernel of its own so that its registers do
+// not cost the hash-chain parser its residency.
+template <bool OPT>
 __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
-    const uint64_t *__restrict__ out_offs, uint32_t n, int attempts, uint8_t *scratch,
-    uint32_t *__restrict__ next_item) {
+    const uint64_t *__restrict__ out_offs, uint32_t n, int attempts, int sufficient,
+    uint8_t *scratch, uint32_t *__restrict__ next_item) {
   HcBlock b;
   b.lane = threadIdx.x;
   uint8_t *sc = scratch + size_t(blockIdx.x) * kHcScratch;
@@ -533,8 +805,11 @@ __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
   b.rank = b.chain + 65536;
   b.sorted = b.rank + 65536;
   b.tr = reinterpret_cast<uint32_t *>(b.sorted + 65536);
+  b.opt = reinterpret_cast<int4 *>(b.tr + 65536);
   b.attempts = attempts;
-  b.pa = attempts > 128;  // lz4hc.c:544
+  // the optimal parser always searches with pattern analysis (lz4hc.c:1267), the
+  // hash-chain parser from level 9 (lz4hc.c:544)
+  b.pa = OPT ? 1 : attempts > 128;
   // Work queue over (block slot, frame) items, slot-major: every wave takes
   // the next item when it finishes one, so the parse's uneven cost per block
   // spreads over the whole grid; the empty slots of short frames come last
@@ -553,7 +828,12 @@ __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
       b.s = reinterpret_cast<uintptr_t>(in) + in_offs[f] + uint64_t(k) * kLz4Block;
       const uintptr_t slot = reinterpret_cast<uintptr_t>(out) + out_offs[f] + 7u + uint64_t(k) * kHcSlot;
       // LZ4_minLength: shorter blocks are all literals and never fit in n-1
-      const int csize = bn >= uint32_t(kLz4MFLimit + 1) ? hc_compress_block(b, slot + 4u, int(bn)) : 0;
+      // (the optimal parser has no such test, but its main loop never runs below 13 bytes
+      // and its last-literals run cannot fit either)
+      int csize = 0;
+      if (bn >= uint32_t(kLz4MFLimit + 1))
+        csize = OPT ? hc_optimal_block(b, slot + 4u, int(bn), sufficient, attempts == 16384)
+                    : hc_compress_block(b, slot + 4u, int(bn));
       if (b.lane == 0) {
         const uint32_t w = csize ? uint32_t(csize) : (bn | 0x80000000u);  // LZ4F_makeBlock
         stb(slot, w & 0xFFu); stb(slot + 1, (w >> 8) & 0xFFu);
@@ -584,11 +864,18 @@ int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const 
   int rc = scratch_acquire(c, kScratchHc, size_t(kHcScratch) * grid + 256, s);
   if (rc) return rc;
   uint8_t *p = c->d_stage[kScratchHc];
-  const int attempts = 1 << (level - 1);  // clTable rows 3..9: 4 .. 256
+  // clTable (lz4hc.c:775-789): nbSearches, and the optimal parser's sufficient length
+  if (level > 12) level = 12;  // MIN(LZ4HC_CLEVEL_MAX, cLevel), lz4hc.c:798
+  const int attempts = level >= 12 ? 16384 : level == 11 ? 512 : level == 10 ? 96 : 1 << (level - 1);
+  const int sufficient = level >= 12 ? kHcOptNum : level == 11 ? 128 : level == 10 ? 64 : 0;
   uint32_t *next_item = reinterpret_cast<uint32_t *>(p + size_t(kHcScratch) * grid);
   RDK_HIP_CHECK(hipMemsetAsync(next_item, 0, sizeof(uint32_t), s));
-  hipLaunchKernelGGL(lz4hc_compress_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
-                     d_in_lens, d_out, d_out_offs, n, attempts, p, next_item);
+  if (sufficient)
+    hipLaunchKernelGGL(lz4hc_compress_blocks_kernel<true>, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
+                       d_in_lens, d_out, d_out_offs, n, attempts, sufficient, p, next_item);
+  else
+    hipLaunchKernelGGL(lz4hc_compress_blocks_kernel<false>, dim3(grid), dim3(64), 0, s, d_in,
+                       d_in_offs, d_in_lens, d_out, d_out_offs, n, attempts, sufficient, p, next_item);
   lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s, nullptr);
   RDK_HIP_CHECK(hipGetLastError());
   return scratch_release(c, kScratchHc, s);

@@ -150,12 +150,6 @@ RDK_API rd_kafka_resp_err_t rd_kafka_lz4_compress(rd_kafka_broker_t *rkb, int pr
   (void)rkb;
   g_calls[CALL_LZ4C]++;
   *outbuf = nullptr;
-  if (comp_level >= 10) {
-    // LZ4HC optimal (lz4hc.c:1278, levels 10..12) is not implemented by the engine
-    slice_drain(slice);
-    set_error(RDK_HIP_E_INVAL, "compression.level %d (LZ4HC optimal) is not implemented", comp_level);
-    return RDK_HIP_RESP_ERR__BAD_COMPRESSION;
-  }
   Ctx *c = ctx();
   if (!c) {
     slice_drain(slice);

@@ -54,8 +54,9 @@ def test_dropin_compress_segments_levels_legacy(engine, oracle_mod):
     assert engine.rd_kafka_lz4_compress(0, 0, data)[1] == \
         oracle_mod.rdk_lz4_compress(data, proper_hc=0)[1]     # broken HC for MsgVersion 0
     s10 = engine.RdSlice(segs)
-    err, _ = engine.rd_kafka_lz4_compress(1, 10, s10)         # LZ4HC optimal: not implemented
-    assert err == engine.RESP_ERR__BAD_COMPRESSION and s10.remains() == 0
+    err, fr = engine.rd_kafka_lz4_compress(1, 10, s10)        # LZ4HC optimal, through segments
+    assert err == 0 and s10.remains() == 0
+    assert fr == oracle_mod.rdk_lz4_compress(data, comp_level=10)[1]
 
 
 def test_dropin_compress_random_shapes(engine, oracle_mod):

@@ -1,4 +1,4 @@
-"""LZ4HC (compression.level 3..9) on the GPU: frames byte-identical to the
+"""LZ4HC (compression.level 3..12) on the GPU: frames byte-identical to the
 reference's LZ4F + lz4hc.c (golden frames from the reference build, and the
 oracle restatement oracle/lz4hc_oracle.c), through the drop-in
 rd_kafka_lz4_compress and the batch API rdk_hip_lz4f_compress."""
@@ -66,7 +66,7 @@ def _pack(items, align=64):
     return buf, offs
 
 
-@pytest.mark.parametrize("level", [3, 5, 7, 9])
+@pytest.mark.parametrize("level", [3, 5, 7, 9, 10, 11, 12])
 def test_batch_hc_matches_oracle(engine, oracle_mod, level):
     import torch
     inputs = _inputs(level)
@@ -88,13 +88,11 @@ def test_batch_hc_matches_oracle(engine, oracle_mod, level):
         assert err == 0 and fr == want, (level, i, len(b), len(fr), len(want))
 
 
-def test_hc_optimal_levels_rejected(engine):
-    import torch
-    d = torch.zeros(1024, dtype=torch.uint8, device="cuda")
-    o = torch.zeros(1, dtype=torch.int64, device="cuda")
-    n = torch.full((1,), 100, dtype=torch.int32, device="cuda")
-    with pytest.raises(engine.EngineError):
-        engine.lz4f_compress_batch(d, o, n, d, o, n, level=10)
+def test_hc_levels_above_12_clamp(engine, oracle_mod):
+    """MIN(LZ4HC_CLEVEL_MAX, cLevel), lz4hc.c:798"""
+    data = W.gen_json(100000, 8)
+    err, fr = engine.rd_kafka_lz4_compress(1, 13, data)
+    assert err == 0 and fr == oracle_mod.rdk_lz4_compress(data, comp_level=12)[1]
 
 
 def test_batch_hc_many_frames_queue_and_scratch_growth(engine, oracle_mod):

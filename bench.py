@@ -991,7 +991,9 @@ def main():
             res["ms"] = t_max
             print(json.dumps({"workload": args.workload, "n_gpus": world, "steps": args.steps,
                               "source_hash": source_hash(),
-                              **leg_line(LEG_NAMES.get(args.workload, args.workload), res,
+                              **leg_line(f"lz4hc_compress_level{args.level}_1MiB_json"
+                                         if args.workload == "lz4hc" else
+                                         LEG_NAMES.get(args.workload, args.workload), res,
                                          args.steps, world, cpu)}), flush=True)
         return finish()
 
@@ -1072,6 +1074,11 @@ def main():
             legs["lz4hc_compress_level9_1MiB_json"] = leg_line(
                 "lz4hc_compress_level9_1MiB_json", bench_lz4c(sub, rank, world, n=256, level=9), 3, 1,
                 cpu("compress", level=9))
+            # LZ4HC optimal parser at its top level (LZ4HC_CLEVEL_MAX = 12)
+            legs["lz4hc_compress_level12_1MiB_json"] = leg_line(
+                "lz4hc_compress_level12_1MiB_json",
+                bench_lz4c(argparse.Namespace(steps=2, warmup=1, partitions=256), rank, world, n=256,
+                           level=12), 2, 1, cpu("compress", level=12))
             legs["consumer_crc_verify_lz4f_decompress_1MiB"] = leg_line(
                 "consumer_crc_verify_lz4f_decompress_1MiB",
                 bench_consumer(argparse.Namespace(steps=3, warmup=1, partitions=1024), rank, world,

@@ -76,12 +76,12 @@ uint32_t rd_slice_crc32(rd_slice_t *slice);
 /* Replaces rd_kafka_lz4_compress() (src/rdkafka_lz4.c:329-442).  LZ4F frame
  * with prefs {blockIndependent, comp_level}, 64 KB blocks; *outbuf is
  * malloc()ed (caller frees with free()); slice is consumed.  comp_level < 3
- * runs LZ4_compress_generic's parse and 3..9 the LZ4HC hash-chain parse
- * (lz4frame.c:797-805), both byte-identical to the reference's frames.
- * comp_level >= 10 (LZ4HC optimal, lz4hc.c:1278) is not implemented:
- * __BAD_COMPRESSION is returned and the writer sends the MessageSet
- * uncompressed (rdkafka_msgset_writer.c:1175).  No call is ever forwarded to
- * another definition of the symbol. */
+ * runs LZ4_compress_generic's parse, 3..9 the LZ4HC hash-chain parse
+ * (lz4frame.c:797-805, lz4hc.c:532) and 10..12 the LZ4HC optimal parse
+ * (lz4hc.c:1278; higher levels clamp to 12, lz4hc.c:798), all byte-identical
+ * to the reference's frames.  A device failure returns __BAD_COMPRESSION (the
+ * writer then sends the MessageSet uncompressed, rdkafka_msgset_writer.c:1175).
+ * No call is ever forwarded to another definition of the symbol. */
 rd_kafka_resp_err_t rd_kafka_lz4_compress(rd_kafka_broker_t *rkb, int proper_hc,
                                           int comp_level, rd_slice_t *slice,
                                           void **outbuf, size_t *outlenp);
@@ -169,7 +169,8 @@ int rdk_hip_msgset_v2_crc(void *d_base, const uint64_t *d_batch_offs,
  * per input, prefs {blockIndependent, level}).  Frame i is written to
  * d_out + d_out_offs[i] (capacity rdk_hip_lz4f_compress_bound(len)); its
  * size goes to d_out_lens[i].  `level` as compression.level: < 3 the fast
- * parse, 3..9 LZ4HC (byte-identical frames); >= 10 is RDK_HIP_E_INVAL. */
+ * parse, 3..9 the LZ4HC hash chain, 10..12 the LZ4HC optimal parser
+ * (byte-identical frames at every level). */
 size_t rdk_hip_lz4f_compress_bound(size_t len);
 int rdk_hip_lz4f_compress(const void *d_in, const uint64_t *d_in_offs,
                           const uint32_t *d_in_lens, void *d_out,

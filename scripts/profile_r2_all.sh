@@ -7,5 +7,6 @@ bash $P crc32c_only_16KiB_batches "crc32c_msgset_v2_v4_kernel" --workload crc --
 bash $P lz4f_compress_1MiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload lz4c --partitions 256 --steps 3 --warmup 1 &&
 bash $P lz4f_compress_fast_1MiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload lz4c_fast --partitions 256 --steps 3 --warmup 1 &&
 bash $P lz4hc_compress_level9_1MiB_json "lz4hc_compress_blocks_kernel,lz4f_assemble_kernel" --workload lz4hc --partitions 256 --steps 3 --warmup 1 &&
+bash $P lz4hc_compress_level12_1MiB_json "lz4hc_compress_blocks_kernel,lz4f_assemble_kernel" --workload lz4hc --level 12 --partitions 256 --steps 2 --warmup 1 &&
 bash $P consumer_crc_verify_lz4f_decompress_1MiB "crc32c_msgset_v2_split_kernel,crc32c_msgset_v2_combine_kernel,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_seq_kernel,lz4f_finish_kernel" --workload consumer --partitions 1024 --steps 3 --warmup 1 &&
 echo PROFILE_ALL_OK

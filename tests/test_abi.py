@@ -91,8 +91,8 @@ def test_dropin_lz4_reports_reference_error_codes_without_a_device():
     err, out = L.rd_kafka_lz4_compress(1, 0, s)
     assert err == L.RESP_ERR__CRIT_SYS_RESOURCE and out == b"" and s.remains() == 0
     s = L.RdSlice([b"abc" * 100])
-    err, out = L.rd_kafka_lz4_compress(1, 12, s)          # LZ4HC optimal: not implemented
-    assert err == L.RESP_ERR__BAD_COMPRESSION and s.remains() == 0
+    err, out = L.rd_kafka_lz4_compress(1, 12, s)          # LZ4HC optimal: the same contract
+    assert err == L.RESP_ERR__CRIT_SYS_RESOURCE and out == b"" and s.remains() == 0
     frame = bytes([0x04, 0x22, 0x4D, 0x18, 0x60, 0x40, 0x82, 0, 0, 0, 0])
     assert L.rd_kafka_lz4_decompress(1, 0, frame) == (L.RESP_ERR__CRIT_SYS_RESOURCE, b"")
 

@@ -57,6 +57,17 @@ def lib():
                                            C.c_size_t, C.c_int]
         L.or_xxh32.restype = C.c_uint32
         L.or_xxh32.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32]
+        L.or_snappy_max_compressed_length.restype = C.c_size_t
+        L.or_snappy_max_compressed_length.argtypes = [C.c_size_t]
+        L.or_snappy_compress.restype = C.c_int
+        L.or_snappy_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.POINTER(C.c_size_t)]
+        L.or_snappy_uncompressed_length.restype = C.c_int
+        L.or_snappy_uncompressed_length.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.or_snappy_uncompress.restype = C.c_int
+        L.or_snappy_uncompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+        L.or_rdk_snappy_decompress.restype = C.c_int
+        L.or_rdk_snappy_decompress.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p),
+                                               C.POINTER(C.c_size_t)]
         L.or_lz4hc_compress_block.restype = C.c_int
         L.or_lz4hc_compress_block.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
         L.or_lz4_compress_block.restype = C.c_int
@@ -187,13 +198,57 @@ def lz4_compress_block(data: bytes, acceleration: int = 1) -> bytes | None:
 
 
 def lz4hc_compress_block(data: bytes, level: int = 9) -> bytes | None:
-    """LZ4HC hash-chain block (levels 3..9, cap = n-1); None means 'stored raw'."""
+    """LZ4HC block (hash chain 3..9, optimal parser 10..12; cap = n-1); None means 'stored raw'."""
     n = len(data)
     src = _buf(data)
     dst = C.create_string_buffer(max(16, n + 16))
     r = lib().or_lz4hc_compress_block(src, n, dst, max(0, n - 1), level)
     assert r >= 0, "level not restated"
     return None if r == 0 else dst.raw[:r]
+
+
+def snappy_max_compressed_length(n: int) -> int:
+    return lib().or_snappy_max_compressed_length(n)
+
+
+def snappy_compress(data: bytes) -> bytes:
+    """rd_kafka_snappy_compress_iov restated: varint length + 64 KiB fragments."""
+    n = len(data)
+    src = _buf(data)
+    dst = C.create_string_buffer(snappy_max_compressed_length(n))
+    out = C.c_size_t(0)
+    assert lib().or_snappy_compress(src, n, dst, C.byref(out)) == 0
+    return dst.raw[:out.value]
+
+
+def snappy_uncompressed_length(data: bytes) -> int | None:
+    b = _buf(data)
+    r = C.c_size_t(0)
+    return r.value if lib().or_snappy_uncompressed_length(b, len(data), C.byref(r)) else None
+
+
+def snappy_uncompress(data: bytes) -> tuple[int, bytes]:
+    """rd_kafka_snappy_uncompress restated: (0, payload) or (-EIO, b"")."""
+    n = snappy_uncompressed_length(data)
+    if n is None:
+        return -5, b""
+    b = _buf(data)
+    out = C.create_string_buffer(max(1, n))
+    r = lib().or_snappy_uncompress(b, len(data), out)
+    return (0, out.raw[:n]) if r == 0 else (r, b"")
+
+
+def rdk_snappy_decompress(data: bytes) -> tuple[int, bytes]:
+    """The reader's snappy case (snappy-java framing or bare): (err, payload)."""
+    b = _buf(data)
+    out = C.c_void_p()
+    n = C.c_size_t(0)
+    err = lib().or_rdk_snappy_decompress(b, len(data), C.byref(out), C.byref(n))
+    if err:
+        return err, b""
+    payload = C.string_at(out, n.value)
+    lib().or_free(out)
+    return 0, payload
 
 
 def lz4_decompress_block(block: bytes, capacity: int, history: bytes = b"") -> tuple[int, bytes]:

@@ -64,8 +64,8 @@ int or_lz4_decompress_block(const uint8_t *src, int csize, uint8_t *dst,
                             int dst_cap, int dict_size);
 /* LZ4HC hash chain (lz4hc_oracle.c): LZ4HC_compress_hashChain (lz4hc.c:532-746)
  * as LZ4F_compressBlockHC (lz4frame.c:782) reaches it for levels 3..9: fresh
- * window per block, limitedOutput.  Returns the size, 0 if it does not fit,
- * -1 for levels >= 10 (LZ4HC_compress_optimal, not restated). */
+ * window per block, limitedOutput, and LZ4HC_compress_optimal (lz4hc.c:1278)
+ * for levels 10..12.  Returns the size, or 0 if it does not fit. */
 int or_lz4hc_compress_block(const uint8_t *src, int n, uint8_t *dst, int dst_cap, int level);
 /* nbSearches of clTable (lz4hc.c:775-789) for a hash-chain level */
 int or_lz4hc_attempts(int level);
@@ -140,6 +140,19 @@ long or_msgset_v01_crc(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32
 /* same walk, CRC through the system zlib (the reference's crc32): the CPU baseline */
 long or_msgset_v01_crc_zlib(uint8_t *set, size_t len, int mode, uint32_t *pos, uint32_t *out,
                             long max_rows);
+
+/* ---- snappy (snappy_oracle.c; parity unpinned, see its header) ------------ */
+/* rd_kafka_snappy_max_compressed_length (snappy.c:639) */
+size_t or_snappy_max_compressed_length(size_t n);
+/* rd_kafka_snappy_compress_iov (snappy.c:1488) over one contiguous input */
+int or_snappy_compress(const uint8_t *src, size_t n, uint8_t *dst, size_t *outlen);
+/* rd_kafka_snappy_uncompressed_length (snappy.c:751): 1 ok, 0 failure */
+int or_snappy_uncompressed_length(const uint8_t *p, size_t n, size_t *result);
+/* rd_kafka_snappy_uncompress (snappy.c:1572): 0 or -EIO */
+int or_snappy_uncompress(const uint8_t *p, size_t n, uint8_t *out);
+/* the reader's snappy case (rdkafka_msgset_reader.c:299-390), snappy-java framing
+ * included: 0 and a malloc()ed payload (or_free), or an OR_ERR_ code */
+int or_rdk_snappy_decompress(const uint8_t *in, size_t inlen, uint8_t **out, size_t *outlen);
 
 #ifdef __cplusplus
 }

@@ -101,6 +101,32 @@ rd_kafka_resp_err_t rd_kafka_lz4_decompress(rd_kafka_broker_t *rkb, int proper_h
  * RDK_HIP_REPORT=1 in the environment the same counts are printed on stderr at exit. */
 void rdk_hip_dropin_calls(uint64_t out[5]);
 
+/* ---- snappy drop-ins (src/snappy.h).  Same signatures, return values and ownership as
+ * the reference's definitions in src/snappy.c; the writer reaches them from
+ * rd_kafka_msgset_writer_compress_snappy (rdkafka_msgset_writer.c:1041-1083), the reader
+ * from its snappy case (rdkafka_msgset_reader.c:299-390).  Streams are byte-identical to
+ * compress_fragment's (snappy.c:957); the decoder returns 0 / -EIO under the conditions
+ * of decompress_all_tags (snappy.c:1226) and writer_append* (:543, :572).  The
+ * environment carries no state here (the hash table lives in LDS). */
+struct snappy_env;
+struct iovec;
+int rd_kafka_snappy_init_env(struct snappy_env *env);                 /* snappy.c:1809 */
+int rd_kafka_snappy_init_env_sg(struct snappy_env *env, bool sg);     /* snappy.c:1778 */
+void rd_kafka_snappy_free_env(struct snappy_env *env);                /* snappy.c:1825 */
+size_t rd_kafka_snappy_max_compressed_length(size_t source_len);      /* snappy.c:639 */
+bool rd_kafka_snappy_uncompressed_length(const char *buf, size_t len, size_t *result); /* :751 */
+int rd_kafka_snappy_compress_iov(struct snappy_env *env, const struct iovec *iov_in,
+                                 size_t iov_in_cnt, size_t input_length,
+                                 struct iovec *iov_out);              /* snappy.c:1488 */
+int rd_kafka_snappy_compress(struct snappy_env *env, const char *input, size_t input_length,
+                             char *compressed, size_t *compressed_length); /* snappy.c:1526 */
+int rd_kafka_snappy_uncompress(const char *compressed, size_t n, char *uncompressed); /* :1572 */
+char *rd_kafka_snappy_java_uncompress(const char *inbuf, size_t inlen, size_t *outlenp,
+                                      char *errstr, size_t errstr_size);  /* snappy.c:1588 */
+/* calls of the snappy drop-ins so far: [0] compress, [1] uncompress (bare or snappy-java);
+ * no counterpart in the reference (see rdk_hip_dropin_calls) */
+void rdk_hip_snappy_dropin_calls(uint64_t out[2]);
+
 /* ------------------------------------------------------------- engine API */
 #define RDK_HIP_OK 0
 #define RDK_HIP_E_NODEV (-1)      /* no usable gfx950 device / code object */
@@ -176,6 +202,30 @@ int rdk_hip_lz4f_compress(const void *d_in, const uint64_t *d_in_offs,
                           const uint32_t *d_in_lens, void *d_out,
                           const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, int level, void *stream);
+
+/* snappy compression of n independent inputs (rd_kafka_snappy_compress_iov semantics per
+ * input, snappy.c:1488): stream i = varint32 length + the 64 KiB fragments of
+ * compress_fragment (snappy.c:957), byte-identical to the reference's, written to
+ * d_out + d_out_offs[i] (capacity rdk_hip_snappy_max_compressed_length(len), which is
+ * also used as staging room); its size goes to d_out_lens[i]. */
+size_t rdk_hip_snappy_max_compressed_length(size_t len);
+int rdk_hip_snappy_compress(const void *d_in, const uint64_t *d_in_offs,
+                            const uint32_t *d_in_lens, void *d_out,
+                            const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                            uint32_t n, void *stream);
+/* snappy decompression of n streams (rd_kafka_snappy_uncompress semantics per stream,
+ * snappy.c:1572): d_out_lens[i] = the length the preamble declares, d_status[i] = 0 or
+ * RDK_HIP_SNAPPY_E_IO (-EIO, the reference's verdict), or RDK_HIP_SNAPPY_E_DSTSIZE when
+ * d_out_caps[i] is below the declared length (the reader sizes its buffer from
+ * rd_kafka_snappy_uncompressed_length first, rdkafka_msgset_reader.c:345-361).  The
+ * chunks of a snappy-java frame (snappy.c:1588) are n streams of one call. */
+#define RDK_HIP_SNAPPY_E_IO (-5)
+#define RDK_HIP_SNAPPY_E_DSTSIZE (-1001)
+int rdk_hip_snappy_uncompress(const void *d_in, const uint64_t *d_in_offs,
+                              const uint32_t *d_in_lens, void *d_out,
+                              const uint64_t *d_out_offs, const uint32_t *d_out_caps,
+                              uint32_t *d_out_lens, int32_t *d_status, uint32_t n,
+                              void *stream);
 
 /* Throughput-mode LZ4F compression: same arguments, frame format, prefs
  * ({blockIndependent}, 64 KB blocks, no checksums) and raw-block fallback

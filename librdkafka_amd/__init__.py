@@ -52,7 +52,12 @@ EXPORTED_SYMBOLS = (
     "rdk_hip_gen_json", "rdk_hip_msgset_v2_sizes", "rdk_hip_msgset_v2_write",
     "rdk_hip_msgset_v2_index", "rd_slice_crc32", "rdk_hip_crc32_ranges",
     "rdk_hip_msgset_v01_crc", "rdk_hip_lz4f_decompress_noalloc", "rdk_hip_msgset_v2_finalize",
-    "rdk_hip_dropin_calls",
+    "rdk_hip_dropin_calls", "rdk_hip_snappy_max_compressed_length", "rdk_hip_snappy_compress",
+    "rdk_hip_snappy_uncompress", "rd_kafka_snappy_init_env", "rd_kafka_snappy_init_env_sg",
+    "rd_kafka_snappy_free_env", "rd_kafka_snappy_max_compressed_length",
+    "rd_kafka_snappy_uncompressed_length", "rd_kafka_snappy_compress_iov",
+    "rd_kafka_snappy_compress", "rd_kafka_snappy_uncompress", "rd_kafka_snappy_java_uncompress",
+    "rdk_hip_snappy_dropin_calls",
 )
 
 
@@ -372,6 +377,96 @@ def lz4f_decompress_batch(src, in_offs, in_lens, dst, out_offs, out_caps, out_le
 
 
 LZ4F_NOALLOC_MAX_FRAMES = 1024
+
+
+# ------------------------------------------------------------------ snappy
+SNAPPY_E_IO, SNAPPY_E_DSTSIZE = -5, -1001
+
+
+def snappy_max_compressed_length(n: int) -> int:
+    f = lib().rdk_hip_snappy_max_compressed_length
+    f.restype, f.argtypes = C.c_size_t, [C.c_size_t]
+    return f(n)
+
+
+def snappy_compress_batch(src, in_offs, in_lens, dst, out_offs, out_lens, stream=None) -> None:
+    """rdk_hip_snappy_compress: n device-resident inputs -> n snappy streams."""
+    _check(lib().rdk_hip_snappy_compress(_ptr(src), _ptr(in_offs), _ptr(in_lens), _ptr(dst),
+                                         _ptr(out_offs), _ptr(out_lens), int(in_offs.numel()),
+                                         _stream(stream)), "snappy_compress")
+
+
+def snappy_uncompress_batch(src, in_offs, in_lens, dst, out_offs, out_caps, out_lens, status,
+                            stream=None) -> None:
+    """rdk_hip_snappy_uncompress: n device-resident streams -> payloads + per-stream verdict."""
+    _check(lib().rdk_hip_snappy_uncompress(_ptr(src), _ptr(in_offs), _ptr(in_lens), _ptr(dst),
+                                           _ptr(out_offs), _ptr(out_caps), _ptr(out_lens),
+                                           _ptr(status), int(in_offs.numel()), _stream(stream)),
+           "snappy_uncompress")
+
+
+class _Iovec(C.Structure):
+    _fields_ = [("iov_base", C.c_void_p), ("iov_len", C.c_size_t)]
+
+
+def rd_kafka_snappy_compress_iov(segments) -> tuple[int, bytes]:
+    """Drop-in rd_kafka_snappy_compress_iov over host segments, driven as
+    rd_kafka_msgset_writer_compress_snappy does (rdkafka_msgset_writer.c:1041-1083):
+    (0, stream) or (negative errno, b"")."""
+    L = lib()
+    segs = [bytes(s) for s in ([segments] if isinstance(segments, (bytes, bytearray)) else segments)]
+    total = sum(len(s) for s in segs)
+    bufs = [C.create_string_buffer(s, max(1, len(s))) for s in segs]
+    iov = (_Iovec * max(1, len(segs)))()
+    for i, (b, s) in enumerate(zip(bufs, segs)):
+        iov[i].iov_base, iov[i].iov_len = C.addressof(b), len(s)
+    env = (C.c_void_p * 3)()
+    L.rd_kafka_snappy_init_env_sg.argtypes = [C.c_void_p, C.c_bool]
+    L.rd_kafka_snappy_init_env_sg(env, True)
+    L.rd_kafka_snappy_max_compressed_length.restype = C.c_size_t
+    L.rd_kafka_snappy_max_compressed_length.argtypes = [C.c_size_t]
+    cap = L.rd_kafka_snappy_max_compressed_length(total)
+    out = C.create_string_buffer(cap)
+    ciov = _Iovec(C.addressof(out), cap)
+    L.rd_kafka_snappy_compress_iov.restype = C.c_int
+    L.rd_kafka_snappy_compress_iov.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
+                                               C.c_void_p]
+    r = L.rd_kafka_snappy_compress_iov(env, iov, len(segs), total, C.byref(ciov))
+    L.rd_kafka_snappy_free_env.argtypes = [C.c_void_p]
+    L.rd_kafka_snappy_free_env(env)
+    return (0, out.raw[:ciov.iov_len]) if r == 0 else (r, b"")
+
+
+def rd_kafka_snappy_decompress(data: bytes) -> tuple[int, bytes]:
+    """The reader's snappy case (rdkafka_msgset_reader.c:299-390) over the drop-in symbols:
+    snappy-java framing or a bare stream.  (0, payload) or (RESP_ERR__BAD_COMPRESSION, b"")."""
+    L = lib()
+    data = bytes(data)
+    buf = C.create_string_buffer(data, max(1, len(data)))
+    if len(data) > 16 + 4 and data[:8] == b"\x82SNAPPY\x00":
+        L.rd_kafka_snappy_java_uncompress.restype = C.c_void_p
+        L.rd_kafka_snappy_java_uncompress.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
+                                                      C.c_char_p, C.c_size_t]
+        n = C.c_size_t(0)
+        err = C.create_string_buffer(128)
+        p = L.rd_kafka_snappy_java_uncompress(C.addressof(buf) + 16, len(data) - 16, C.byref(n),
+                                              err, 128)
+        if not p:
+            return RESP_ERR__BAD_COMPRESSION, b""
+        out = C.string_at(p, n.value)
+        _libc().free(p)
+        return 0, out
+    L.rd_kafka_snappy_uncompressed_length.restype = C.c_bool
+    L.rd_kafka_snappy_uncompressed_length.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    n = C.c_size_t(0)
+    if not L.rd_kafka_snappy_uncompressed_length(buf, len(data), C.byref(n)):
+        return RESP_ERR__BAD_COMPRESSION, b""
+    out = C.create_string_buffer(max(1, n.value))
+    L.rd_kafka_snappy_uncompress.restype = C.c_int
+    L.rd_kafka_snappy_uncompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+    if L.rd_kafka_snappy_uncompress(buf, len(data), out):
+        return RESP_ERR__BAD_COMPRESSION, b""
+    return 0, out.raw[:n.value]
 
 
 def lz4f_decompress_batch_noalloc(src, in_offs, in_lens, dst, out_offs, out_caps, out_lens,

@@ -1,0 +1,647 @@
+// snappy.hip -- snappy compression and decompression on gfx950.
+//
+// Replaces, for whole batches of MessageSets at a time, the codec behind
+// rd_kafka_msgset_writer_compress_snappy (rdkafka_msgset_writer.c:1041) =
+// rd_kafka_snappy_compress_iov (snappy.c:1488) -> sn_compress (:1408) ->
+// compress_fragment (:957), and behind the reader's snappy case
+// (rdkafka_msgset_reader.c:299-390) = rd_kafka_snappy_uncompress (snappy.c:1572)
+// -> decompress_all_tags (:1226).
+//
+// COMPRESS.  sn_compress cuts the input into 64 KiB fragments and zeroes the hash
+// table for each (get_hash_table, snappy.c:790), so fragments are independent: one
+// wavefront per fragment, its u16 table (up to 2^14 entries, 32 KiB) in LDS.
+// compress_fragment's greedy parse is emulated exactly, so streams are byte-identical
+// to snappy.c's:
+//   * the search evaluates 64 consecutive probes at once; the skip schedule
+//     (bytes_between_hash_lookups = skip++ >> 5, :1019) is reproduced by a lane prefix
+//     sum; a probe's candidate is the latest earlier probe of the step with the same
+//     hash (14 ballots) or else the table entry; the first verifying probe wins and
+//     only probes up to it update the table, last writer per hash;
+//   * find_match_length, the literal copy and the copy elements of long matches
+//     (emit_copy, :718) move 64 bytes / write 64 elements per wave step;
+//   * after a copy the table takes ip-1 and the position behind the copy is tested at
+//     once (:1071-1088).
+// Fragment k of stream f is compressed into a slot of the caller's output buffer
+// (4-byte size + payload; a fragment of this compressor grows by at most 1/64 + 8
+// bytes, so the slots fit rd_kafka_snappy_max_compressed_length); an assemble kernel
+// writes the varint32 length and slides the fragments together.
+//
+// DECOMPRESS.  A snappy stream has no block index, so one wavefront decodes one
+// stream, 64 compressed bytes per step, with the discovery / pointer-doubling walk /
+// lane-per-byte expansion scheme of the LZ4 block decoder (lz4_decode_fast.h): every
+// lane parses the element that would start at its byte (tag + up to 3 bytes), the
+// real elements are the orbit of the entry position under "next element", and the
+// output is painted 64 bytes at a time from the input (literals), the wave's LDS
+// history ring, or the already written output.  Elements whose header needs a fifth
+// byte (literals of 16 MiB and more, 4-byte offsets) are parsed by a scalar routine.
+// Every condition under which decompress_all_tags / writer_append* fail is checked
+// (offset 0 or beyond the produced bytes, output or input overrun, a length that
+// does not match the preamble), so the verdict is the reference's: 0 or -EIO.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "lz4_device.h"
+
+namespace rdk {
+
+typedef __attribute__((address_space(3))) uint16_t sn_lds_u16;
+typedef __attribute__((address_space(3))) uint8_t sn_lds_u8;
+typedef __amdgpu_buffer_rsrc_t sn_rsrc_t;
+
+constexpr uint32_t kSnBlock = 65536;          // kblock_size, snappy.c:774
+constexpr uint32_t kSnMaxTable = 1u << 14;    // kmax_hash_table_size, snappy.c:781
+constexpr uint32_t kSnSlot = kSnBlock + 2048; // bytes per staged fragment (size word + payload)
+constexpr uint32_t kSnSlot0 = 8;              // room for the varint32 in front of slot 0
+constexpr int kSnItems = 64;                  // fragment slots per stream per pass
+constexpr uint32_t kSnMul = 0x1e35a7bdu;      // hash_bytes, snappy.c:606
+constexpr int kSnEIO = -5;
+constexpr int kSnDstSize = -1001;             // RDK_HIP_SNAPPY_E_DSTSIZE
+
+__device__ __forceinline__ uint32_t sn_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(v, d);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+// equal bytes a[i] == b[i], i < limit, 64 per wave step (find_match_length, snappy.c:823)
+__device__ __forceinline__ uint32_t sn_count(uintptr_t a, uintptr_t b, uint32_t limit, int lane) {
+  uint32_t cnt = 0;
+  while (cnt < limit) {
+    const uint32_t l = cnt + uint32_t(lane);
+    const bool ok = l < limit && ldb(a + l) == ldb(b + l);
+    const uint64_t m = ballot(ok);
+    const uint32_t run = m == ~0ull ? 64u : uint32_t(__builtin_ctzll(~m));
+    cnt += run;
+    if (run < 64u) break;
+  }
+  return cnt;
+}
+
+__device__ __forceinline__ void sn_copy(uintptr_t d, uintptr_t s, uint32_t len, int lane) {
+  for (uint32_t base = 0; base < len; base += 256u) {
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = base + uint32_t(lane) + 64u * j;
+      v[j] = i < len ? ldb(s + i) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = base + uint32_t(lane) + 64u * j;
+      if (i < len) stb(d + i, v[j]);
+    }
+  }
+}
+
+// emit_literal (snappy.c:652-695): returns the bytes written
+__device__ __forceinline__ uint32_t sn_emit_literal(uintptr_t d, uintptr_t lit, uint32_t len, int lane) {
+  const uint32_t n = len - 1u;
+  uint32_t hdr;
+  if (n < 60u) {
+    hdr = 1u;
+    if (lane == 0) stb(d, n << 2);
+  } else {
+    const uint32_t count = n < 0x100u ? 1u : n < 0x10000u ? 2u : n < 0x1000000u ? 3u : 4u;
+    hdr = 1u + count;
+    if (lane == 0) stb(d, (59u + count) << 2);
+    if (uint32_t(lane) < count) stb(d + 1u + uint32_t(lane), (n >> (8u * uint32_t(lane))) & 0xFFu);
+  }
+  sn_copy(d + hdr, lit, len, lane);
+  return hdr + len;
+}
+
+// emit_copy (snappy.c:718-741): 64-byte copies while 68 or more remain, a 60-byte copy when
+// 65..67 remain, then the rest (emit_copy_less_than64, :697).  Returns the bytes written.
+__device__ __forceinline__ uint32_t sn_emit_copy(uintptr_t d, uint32_t offset, uint32_t len, int lane) {
+  const uint32_t k64 = len >= 68u ? (len - 4u) / 64u : 0u;
+  for (uint32_t j = uint32_t(lane); j < k64; j += 64u) {
+    stb(d + 3u * j, 2u + (63u << 2));
+    stb(d + 3u * j + 1u, offset & 0xFFu);
+    stb(d + 3u * j + 2u, offset >> 8);
+  }
+  uint32_t o = 3u * k64, rem = len - 64u * k64;
+  if (lane == 0) {
+    if (rem > 64u) {
+      stb(d + o, 2u + (59u << 2));
+      stb(d + o + 1u, offset & 0xFFu);
+      stb(d + o + 2u, offset >> 8);
+    }
+  }
+  if (rem > 64u) { o += 3u; rem -= 60u; }
+  const bool small = rem < 12u && offset < 2048u;
+  if (lane == 0) {
+    if (small) {
+      stb(d + o, 1u + ((rem - 4u) << 2) + ((offset >> 8) << 5));
+      stb(d + o + 1u, offset & 0xFFu);
+    } else {
+      stb(d + o, 2u + ((rem - 1u) << 2));
+      stb(d + o + 1u, offset & 0xFFu);
+      stb(d + o + 2u, offset >> 8);
+    }
+  }
+  return o + (small ? 2u : 3u);
+}
+
+// compress_fragment (snappy.c:957-1103).  table[0, tsize) is zero.  Returns the size.
+__device__ uint32_t sn_compress_fragment(uintptr_t src, uint32_t n, uintptr_t dst, sn_lds_u16 *table,
+                                         uint32_t tsize, int lane) {
+  const uint32_t shift = 32u - uint32_t(31 - __builtin_clz(tsize));
+  uint32_t ip = 0, next_emit = 0, op = 0;
+  if (n >= 15u) {
+    const uint32_t ip_limit = n - 15u;
+    ip = 1;
+    bool running = true;
+    while (running) {
+      // ---- step 1: scan forward for a 4-byte match (:1011-1031)
+      uint32_t cand = 0;
+      {
+        uint32_t fwd = ip, cbase = 0;
+        for (;;) {
+          const uint32_t c = cbase + uint32_t(lane);
+          const uint32_t s = (32u + c) >> 5;
+          const uint32_t incl = sn_incl_scan(s, lane);
+          const uint32_t P = fwd + incl - s, Pn = fwd + incl;
+          const bool valid = Pn <= ip_limit;  // next_ip > ip_limit ends the fragment (:1021)
+          const uint64_t vmask = ballot(valid);
+          const uint32_t seq = valid ? ld32u(src + P) : 0u;
+          const uint32_t h = (seq * kSnMul) >> shift;
+          uint64_t eq = vmask;
+#pragma unroll
+          for (uint32_t bit = 0; bit < 14u; ++bit) {
+            const bool hb = (h >> bit) & 1u;
+            const uint64_t bm = ballot(hb);
+            eq &= hb ? bm : ~bm;
+          }
+          const uint64_t lower = eq & ((1ull << lane) - 1ull);
+          const int pred = lower ? 63 - __builtin_clzll(lower) : 0;
+          const uint32_t predP = uint32_t(__shfl(int(P), pred));
+          const uint32_t cd = lower ? predP : uint32_t(table[h]);
+          const bool m = valid && ld32u(src + cd) == seq;
+          const uint64_t mm = ballot(m);
+          const int f = mm ? __builtin_ctzll(mm) : 64;
+          const int e = ~vmask ? __builtin_ctzll(~vmask) : 64;
+          if (f < e) {
+            const uint64_t upto = (2ull << f) - 1ull;
+            const uint64_t later = eq & ~((2ull << lane) - 1ull) & upto;
+            if (lane <= f && !later) table[h] = uint16_t(P);
+            ip = uint32_t(__builtin_amdgcn_readlane(int(P), f));
+            cand = uint32_t(__builtin_amdgcn_readlane(int(cd), f));
+            break;
+          }
+          if (e < 64) { running = false; break; }
+          {
+            const uint64_t later = eq & ~((2ull << lane) - 1ull);
+            if (!later) table[h] = uint16_t(P);
+          }
+          fwd = uint32_t(__builtin_amdgcn_readlane(int(Pn), 63));
+          cbase += 64u;
+        }
+      }
+      if (!running) break;
+      asm volatile("" ::: "memory");
+      // ---- step 2: the bytes before the match are a literal (:1039)
+      op += sn_emit_literal(dst + op, src + next_emit, ip - next_emit, lane);
+      // ---- step 3: copies while the position behind the last copy matches (:1054-1088)
+      for (;;) {
+        const uint32_t matched = 4u + sn_count(src + cand + 4u, src + ip + 4u, n - (ip + 4u), lane);
+        op += sn_emit_copy(dst + op, ip - cand, matched, lane);
+        ip += matched;
+        next_emit = ip;
+        if (ip >= ip_limit) { running = false; break; }
+        const uint32_t h1 = (ld32u(src + ip - 1u) * kSnMul) >> shift;
+        if (lane == 0) table[h1] = uint16_t(ip - 1u);
+        asm volatile("" ::: "memory");
+        const uint32_t seq = ld32u(src + ip);
+        const uint32_t h = (seq * kSnMul) >> shift;
+        const uint32_t mi = uni(uint32_t(table[h]));
+        asm volatile("" ::: "memory");
+        if (lane == 0) table[h] = uint16_t(ip);
+        asm volatile("" ::: "memory");
+        if (ld32u(src + mi) == seq) { cand = mi; continue; }
+        ip++;
+        break;
+      }
+    }
+  }
+  if (next_emit < n) op += sn_emit_literal(dst + op, src + next_emit, n - next_emit, lane);  // :1097
+  return op;
+}
+
+// One wavefront per fragment; items are slot-major so that every shader engine is busy.
+__global__ __launch_bounds__(64) void snappy_compress_fragments_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
+    const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
+    const uint64_t *__restrict__ out_offs, uint32_t n) {
+  __shared__ uint16_t table_mem[kSnMaxTable];
+  sn_lds_u16 *table = (sn_lds_u16 *)table_mem;
+  const int lane = threadIdx.x;
+  const uint32_t items = n * uint32_t(kSnItems);
+  for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const uint32_t f = it % n, kk = it / n;
+    const uint32_t len = uni(in_lens[f]);
+    const uint32_t nb = (len + kSnBlock - 1u) / kSnBlock;
+    for (uint32_t k = kk; k < nb; k += uint32_t(kSnItems)) {
+      const uint32_t fn = len - k * kSnBlock < kSnBlock ? len - k * kSnBlock : kSnBlock;
+      uint32_t tsize = 256;  // get_hash_table, snappy.c:790-807
+      while (tsize < kSnMaxTable && tsize < fn) tsize <<= 1;
+      for (uint32_t i = uint32_t(lane); i < tsize; i += 64u) table[i] = 0;
+      asm volatile("" ::: "memory");
+      const uintptr_t src = reinterpret_cast<uintptr_t>(in) + in_offs[f] + uint64_t(k) * kSnBlock;
+      const uintptr_t slot =
+          reinterpret_cast<uintptr_t>(out) + out_offs[f] + kSnSlot0 + uint64_t(k) * kSnSlot;
+      const uint32_t sz = sn_compress_fragment(src, fn, slot + 4u, table, tsize, lane);
+      if (lane == 0) {
+        stb(slot, sz & 0xFFu); stb(slot + 1, (sz >> 8) & 0xFFu);
+        stb(slot + 2, (sz >> 16) & 0xFFu); stb(slot + 3, sz >> 24);
+      }
+    }
+  }
+}
+
+// One workgroup per stream: the varint32 of the input length (varint_encode32, snappy.c:297),
+// then the fragments slid together (destination always below source).
+__global__ __launch_bounds__(256) void snappy_assemble_kernel(
+    const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
+    uint32_t *__restrict__ out_lens, uint32_t n) {
+  const int t = threadIdx.x;
+  for (uint32_t f = blockIdx.x; f < n; f += gridDim.x) {
+    const uint32_t len = in_lens[f];
+    const uint32_t nb = (len + kSnBlock - 1u) / kSnBlock;
+    const uintptr_t ob = reinterpret_cast<uintptr_t>(out) + out_offs[f];
+    uint32_t vl = 1;
+    for (uint32_t v = len; v >= 128u; v >>= 7) vl++;
+    uint64_t pos = vl;
+    for (uint32_t k = 0; k < nb; ++k) {
+      const uintptr_t slot = ob + kSnSlot0 + uint64_t(k) * kSnSlot;
+      const uint32_t sz = ldb(slot) | (ldb(slot + 1) << 8) | (ldb(slot + 2) << 16) | (ldb(slot + 3) << 24);
+      __syncthreads();  // everyone has read the size word before it may be overwritten
+      const uintptr_t from = slot + 4u, to = ob + pos;
+      for (uint32_t base = 0; base < sz; base += 256u * 16u) {
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const uint32_t i = base + uint32_t(t) + 256u * j;
+          v[j] = i < sz ? ldb(from + i) : 0u;
+        }
+        __syncthreads();  // chunk fully read before any lane writes (dst < src)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const uint32_t i = base + uint32_t(t) + 256u * j;
+          if (i < sz) stb(to + i, v[j]);
+        }
+        __syncthreads();
+      }
+      pos += sz;
+    }
+    if (t == 0) {
+      uint32_t v = len, i = 0;
+      for (; v >= 128u; v >>= 7) stb(ob + i++, (v & 127u) | 128u);
+      stb(ob + i, v);
+      out_lens[f] = uint32_t(pos);
+    }
+    __syncthreads();
+  }
+}
+
+// ===================================================================== decompress
+constexpr uint32_t kSnRing = 4096;            // LDS history per wavefront
+constexpr uint32_t kSnRingMask = kSnRing - 1u;
+constexpr int kSnDecWaves = 4;                // wavefronts per workgroup
+constexpr uint32_t kSnLitTag = 0x80000000u;
+constexpr uint32_t kSnNoAccess = 0x80000000u; // out-of-range buffer offset (reads 0, stores nothing)
+constexpr uint32_t kSnComplex = 0xFFFFFFFFu;  // header needs a fifth byte
+constexpr uint32_t kSnBad = 0xFFFFFFFEu;      // no element can start here
+
+__device__ __forceinline__ sn_rsrc_t sn_make_rsrc(uintptr_t base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), 0, int(bytes), 0x00020000);
+}
+__device__ __forceinline__ uint64_t sn_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+__device__ __forceinline__ uint32_t sn_incl_max(uint32_t v) {
+  int x = int(v);
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true));
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true));
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true));
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true));
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));
+  return uint32_t(x);
+}
+__device__ __forceinline__ uint32_t sn_excl_sum(uint32_t v, uint32_t &total) {
+  int x = int(v);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  total = uint32_t(__builtin_amdgcn_readlane(x, 63));
+  return uint32_t(x) - v;
+}
+
+struct SnDec {
+  sn_lds_u8 *ring, *map;  // map: [0, 64) per-piece scratch, [64, 128) stores of parked lanes
+  // rin spans the whole dwords that hold the stream (a range-checked dword that is only
+  // partly inside a buffer reads as zero, and a stream may end in a 2-byte element):
+  // offsets into it are stream positions + din
+  sn_rsrc_t rin, rout;
+  uint32_t din;
+  uint32_t pn, poc, plb, pfb, prb;  // the fetched, not yet written piece
+};
+
+__device__ __forceinline__ void sn_retire(SnDec &d, int lane) {
+  const bool live = uint32_t(lane) < d.pn;
+  const uint32_t v = d.plb | d.pfb | d.prb;
+  sn_lds_u8 *slot = live ? d.ring + ((d.poc + uint32_t(lane)) & kSnRingMask) : d.map + 64 + lane;
+  *slot = uint8_t(v);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), d.rout, live ? d.poc + uint32_t(lane) : kSnNoAccess, 0, 0);
+  d.pn = 0;
+}
+
+// fetch output bytes [pc, pc+nvalid): lane l's byte comes from `src` (tag | input position, or
+// an output position below its own)
+__device__ __forceinline__ void sn_flush(SnDec &d, uint32_t src, uint32_t pc, uint32_t nvalid, int lane) {
+  sn_retire(d, lane);
+  const bool live = uint32_t(lane) < nvalid;
+  for (;;) {  // sources inside the piece: pointer jumping (unconditional shuffle, then select)
+    const bool intra = live & (int32_t(src) >= int32_t(pc));
+    if (!sn_ballot(intra)) break;
+    const uint32_t v = uint32_t(__shfl(int(src), int((src - pc) & 63u)));
+    src = intra ? v : src;
+  }
+  const bool lit = int32_t(src) < 0;
+  const uint32_t q = src & ~kSnLitTag;
+  const bool ring_ok = !lit & (q + kSnRing >= pc);
+  const bool far = live & !lit & !ring_ok;
+  d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live & lit) ? q + d.din : kSnNoAccess, 0, 0);
+  d.pfb = __builtin_amdgcn_raw_buffer_load_b8(d.rout, far ? q : kSnNoAccess, 0, 0);
+  asm volatile("" ::: "memory");
+  d.prb = d.ring[q & kSnRingMask] & (ring_ok ? 0xFFu : 0u);
+  d.pn = nvalid;
+  d.poc = pc;
+}
+
+// The element that would start at p = seg + lane, from the 4 bytes at p (char_table,
+// snappy.c:1129): A = next element start (kSnComplex / kSnBad), ll / ml = literal / copy
+// bytes, off = copy offset, k = header bytes.
+struct SnCand {
+  uint32_t A, ll, off, mk;  // mk = ml | k << 8
+};
+
+__device__ __forceinline__ SnCand sn_parse(const SnDec &d, uint32_t csize, uint32_t seg, int lane) {
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  const uint32_t p = seg + uint32_t(lane);
+  const u2 h = __builtin_amdgcn_raw_buffer_load_b64(d.rin, (p + d.din) & ~3u, 0, 0);
+  const uint32_t w = __builtin_amdgcn_alignbyte(h.y, h.x, (p + d.din) & 3u);
+  const uint32_t c = w & 0xFFu, kind = c & 3u, hi = c >> 2;
+  const uint32_t b1 = (w >> 8) & 0xFFu, b12 = (w >> 8) & 0xFFFFu, b123 = w >> 8;
+  const bool islit = kind == 0u;
+  const uint32_t lext = hi >= 60u ? hi - 59u : 0u;  // extra length bytes of a literal
+  const uint32_t k = 1u + (islit ? lext : kind == 1u ? 1u : kind == 2u ? 2u : 4u);
+  const bool complex = (islit & (lext == 4u)) | (kind == 3u);
+  const uint32_t lv = lext == 0u ? hi : lext == 1u ? b1 : lext == 2u ? b12 : b123;
+  const uint32_t ll = islit ? lv + 1u : 0u;
+  const uint32_t ml = islit ? 0u : kind == 1u ? 4u + (hi & 7u) : hi + 1u;
+  const uint32_t off = kind == 1u ? ((c >> 5) << 8) | b1 : b12;
+  SnCand r;
+  const bool bad = (p >= csize) | (p + k > csize);  // refill_tag cannot complete the header
+  r.A = bad ? kSnBad : complex ? kSnComplex : p + k + ll;
+  r.ll = ll;
+  r.off = off;
+  r.mk = ml | (k << 8);
+  return r;
+}
+
+// wave-uniform byte of the stream (slow path only)
+__device__ __forceinline__ uint32_t sn_in_byte(const SnDec &d, uint32_t i) {
+  return __builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b8(d.rin, i + d.din, 0, 0));
+}
+
+// Decode the stream at `src` (n bytes) into `dst` (cap bytes).  Returns 0 or -EIO like
+// rd_kafka_snappy_uncompress; *ulen_out = the declared length (0 when unreadable).
+#ifdef RDK_SN_DEBUG
+#define SN_FAIL(site) (kSnEIO - 100 * (site))
+#else
+#define SN_FAIL(site) kSnEIO
+#endif
+__device__ int sn_decode_stream(uintptr_t src, uint32_t n, uintptr_t dst, uint32_t cap,
+                                uint32_t *ulen_out, sn_lds_u8 *ring, sn_lds_u8 *map, int lane) {
+  if (n >= 0x80000000u) return SN_FAIL(1);  // input positions carry a tag in bit 31
+  SnDec d;
+  d.ring = ring;
+  d.map = map;
+  d.din = uint32_t(src & 3u);
+  d.rin = sn_make_rsrc(src - d.din, (d.din + n + 3u) & ~3u);
+  d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
+  // read_uncompressed_length (snappy.c:1193-1218)
+  uint32_t ulen = 0, ip0 = 0;
+  for (uint32_t shift = 0;; shift += 7u) {
+    if (shift >= 32u || ip0 >= n) return SN_FAIL(2);
+    const uint32_t c = sn_in_byte(d, ip0++);
+    ulen |= (c & 0x7Fu) << shift;
+    if (c < 128u) break;
+  }
+  *ulen_out = ulen;
+  if (ulen > 0x7FFFFFF0u) return SN_FAIL(3);  // positions are kept in 31 bits
+  if (ulen > cap) return kSnDstSize;      // the caller sizes dst from the preamble
+  d.rout = sn_make_rsrc(dst, ulen);
+  uint32_t op = 0, ipn = ip0;
+  if (ipn == n) return ulen == 0u ? 0 : SN_FAIL(21);
+  uint32_t seg = ipn & ~63u;
+  SnCand cur = sn_parse(d, n, seg, lane);
+  SnCand nxt = sn_parse(d, n, seg + 64u, lane);
+  for (;;) {
+    // ---- walk: which candidate lanes are the real elements of this segment
+    const uint32_t x0 = ipn - seg;
+    uint64_t M;
+    for (;;) {
+      const bool stop = (cur.A - seg >= 64u) | (cur.A == n);  // bad, complex, leaves, or ends the stream
+      uint32_t J = stop ? 64u : cur.A - seg;
+      bool R = uint32_t(lane) == x0;
+#pragma unroll
+      for (int level = 0; level < 5; ++level) {
+        const bool send = R & (J < 64u);
+        const int t = __builtin_amdgcn_ds_permute(int((send ? J : x0) << 2), int(send));
+        R = R | (t != 0);
+        const uint32_t jj = uint32_t(__shfl(int(J), int(J & 63u)));
+        J = J < 64u ? jj : 64u;
+      }
+      M = sn_ballot(R);
+      if (sn_ballot(R & (cur.A == kSnBad))) return SN_FAIL(4);
+      const uint64_t cx = sn_ballot(R & (cur.A == kSnComplex));
+      if (!cx) break;
+      // header with a fifth byte: literal of 2^24 bytes or more, or a 4-byte offset
+      const uint32_t xc = uint32_t(__builtin_ctzll(cx));
+      const uint32_t p = seg + xc;
+      const uint32_t c = sn_in_byte(d, p);
+      const uint32_t v = sn_in_byte(d, p + 1u) | (sn_in_byte(d, p + 2u) << 8) |
+                         (sn_in_byte(d, p + 3u) << 16) | (sn_in_byte(d, p + 4u) << 24);
+      const bool me = uint32_t(lane) == xc;
+      if ((c & 3u) == 3u) {  // copy with a 4-byte offset
+        cur.A = me ? p + 5u : cur.A;
+        cur.ll = me ? 0u : cur.ll;
+        cur.off = me ? v : cur.off;
+        cur.mk = me ? ((c >> 2) + 1u) | (5u << 8) : cur.mk;
+      } else {
+        const uint64_t nx = uint64_t(p) + 5u + uint64_t(v) + 1u;
+        if (nx > n) return SN_FAIL(5);  // premature end of input (:1283)
+        cur.A = me ? uint32_t(nx) : cur.A;
+        cur.ll = me ? v + 1u : cur.ll;
+        cur.off = me ? 0u : cur.off;
+        cur.mk = me ? (5u << 8) : cur.mk;
+      }
+    }
+    const uint32_t xl = uint32_t(63 - __builtin_clzll(M));
+    const uint32_t a_last = uni(__builtin_amdgcn_readlane(cur.A, xl));
+    if (a_last > n) return SN_FAIL(6);  // the last literal runs past the input
+    const bool done = a_last == n;
+    // ---- the segment's elements, one per member lane, in lane order
+    const bool mem = (M >> lane) & 1ull;
+    const uint32_t ll = cur.ll, ml = cur.mk & 0xFFu, off = cur.off, k = cur.mk >> 8;
+    const uint32_t len = mem ? ll + ml : 0u;
+    // (the members' literals are disjoint pieces of an input below 2^31 bytes, so the sum of
+    // their lengths cannot wrap)
+    uint32_t T;
+    const uint32_t ostart = op + sn_excl_sum(len, T);
+    if (uint64_t(op) + T > ulen) return SN_FAIL(7);  // writer_append* : no room (:572, :543)
+    // writer_append_from_self: offset 0 or beyond the produced bytes (:548)
+    if (sn_ballot(mem & (ml != 0u) & (ostart <= off - 1u))) return SN_FAIL(8);
+    // ---- output [op, op+T) in pieces of 64 bytes, lane per byte
+    const uint32_t op_new = uni(op + T);
+    const uint32_t ls = seg + uint32_t(lane) + k;  // first literal byte
+    uint32_t carry = 0;
+    for (uint32_t c = op; c < op_new; c = uni(c + 64u)) {
+      map[lane] = 0;
+      asm volatile("" ::: "memory");
+      const uint32_t rel0 = ostart - c;
+      map[((len != 0u) & (rel0 < 64u)) ? rel0 : 64u + uint32_t(lane)] = uint8_t(lane + 1);
+      asm volatile("" ::: "memory");
+      uint32_t v = sn_incl_max(map[lane]);
+      v = v ? v : carry;
+      carry = __builtin_amdgcn_readlane(v, 63);
+      const int idx = int((v - 1u) & 63u);
+      const uint32_t g_os = uint32_t(__shfl(int(ostart), idx));
+      const uint32_t g_ll = uint32_t(__shfl(int(ll), idx));
+      const uint32_t g_ls = uint32_t(__shfl(int(ls), idx));
+      const uint32_t g_of = uint32_t(__shfl(int(off), idx));
+      const uint32_t o = c + uint32_t(lane);
+      const uint32_t rel = o - g_os;
+      const uint32_t s_lit = (g_ls + rel) | kSnLitTag, s_mat = o - g_of;
+      const uint32_t pick = 0u - uint32_t(rel < g_ll);
+      const uint32_t s = (s_lit & pick) | (s_mat & ~pick);
+      const uint32_t left = op_new - c;
+      sn_flush(d, s, c, left < 64u ? left : 64u, lane);
+    }
+    op = op_new;
+    if (done) {
+      sn_retire(d, lane);
+      return op == ulen ? 0 : SN_FAIL(20);  // eof && writer_check_length (:1403)
+    }
+    ipn = a_last;
+    const uint32_t nseg = ipn & ~63u;
+    if (nseg == seg + 64u) {
+      cur = nxt;
+    } else {
+      cur = sn_parse(d, n, nseg, lane);
+    }
+    seg = nseg;
+    nxt = sn_parse(d, n, seg + 64u, lane);
+  }
+}
+
+__global__ __launch_bounds__(64 * kSnDecWaves) void snappy_uncompress_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
+    const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
+    const uint32_t *__restrict__ out_caps, uint32_t *__restrict__ out_lens,
+    int32_t *__restrict__ status, uint32_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t rings[kSnDecWaves][kSnRing];
+  __shared__ __attribute__((aligned(16))) uint8_t maps[kSnDecWaves][128];
+  const int lane = threadIdx.x & 63;
+  const uint32_t w = uni(threadIdx.x >> 6);
+  sn_lds_u8 *ring = (sn_lds_u8 *)rings[w];
+  sn_lds_u8 *map = (sn_lds_u8 *)maps[w];
+  const uint32_t wpb = blockDim.x >> 6;
+  for (uint32_t f = blockIdx.x * wpb + w; f < n; f += gridDim.x * wpb) {
+    const uintptr_t src = reinterpret_cast<uintptr_t>(in) + in_offs[f];
+    const uintptr_t dst = reinterpret_cast<uintptr_t>(out) + out_offs[f];
+    uint32_t ulen = 0;
+    const int r = sn_decode_stream(src, uni(in_lens[f]), dst, uni(out_caps[f]), &ulen, ring, map, lane);
+    if (lane == 0) {
+      status[f] = r;
+      out_lens[f] = ulen;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host side
+size_t snappy_max_compressed_length(size_t len) { return 32 + len + len / 6; }  // snappy.c:639
+
+int snappy_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
+                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                           uint32_t n, hipStream_t s) {
+  if (!n) return 0;
+  if (n > 0xFFFFFFFFu / kSnItems) return set_error(RDK_HIP_E_INVAL, "too many streams");
+  const uint64_t items = uint64_t(n) * kSnItems;
+  const unsigned grid = unsigned(items < 65536u ? items : 65536u);
+  hipLaunchKernelGGL(snappy_compress_fragments_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
+                     d_in_lens, d_out, d_out_offs, n);
+  hipLaunchKernelGGL(snappy_assemble_kernel, dim3(n < 4096u ? n : 4096u), dim3(256), 0, s, d_in_lens,
+                     d_out, d_out_offs, d_out_lens, n);
+  RDK_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int snappy_uncompress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
+                             uint8_t *d_out, const uint64_t *d_out_offs, const uint32_t *d_out_caps,
+                             uint32_t *d_out_lens, int32_t *d_status, uint32_t n, hipStream_t s) {
+  if (!n) return 0;
+  const unsigned wg = (n + kSnDecWaves - 1) / kSnDecWaves;
+  hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(wg < 2048u ? wg : 2048u), dim3(64 * kSnDecWaves), 0,
+                     s, d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_caps, d_out_lens, d_status,
+                     n);
+  RDK_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace rdk
+
+using namespace rdk;
+
+// rd_kafka_snappy_max_compressed_length (snappy.c:639)
+RDK_API size_t rdk_hip_snappy_max_compressed_length(size_t len) {
+  return snappy_max_compressed_length(len);
+}
+
+RDK_API int rdk_hip_snappy_compress(const void *d_in, const uint64_t *d_in_offs,
+                                    const uint32_t *d_in_lens, void *d_out,
+                                    const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
+                                    void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_in || !d_in_offs || !d_in_lens || !d_out || !d_out_offs || !d_out_lens)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  return snappy_compress_device(static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
+                                static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n,
+                                static_cast<hipStream_t>(stream));
+}
+
+RDK_API int rdk_hip_snappy_uncompress(const void *d_in, const uint64_t *d_in_offs,
+                                      const uint32_t *d_in_lens, void *d_out,
+                                      const uint64_t *d_out_offs, const uint32_t *d_out_caps,
+                                      uint32_t *d_out_lens, int32_t *d_status, uint32_t n,
+                                      void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_in || !d_in_offs || !d_in_lens || !d_out || !d_out_offs || !d_out_caps || !d_out_lens ||
+      !d_status)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  return snappy_uncompress_device(static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
+                                  static_cast<uint8_t *>(d_out), d_out_offs, d_out_caps, d_out_lens,
+                                  d_status, n, static_cast<hipStream_t>(stream));
+}

@@ -1,0 +1,181 @@
+"""snappy on the GPU (csrc/snappy.hip): streams byte-identical to the restatement of
+snappy.c's compress_fragment (oracle/snappy_oracle.c; its parity with snappy.c itself is
+unpinned, see that file), decodable by an independent snappy (pyarrow's), and a decoder whose
+verdicts (0 / -EIO) and payloads equal the oracle's on valid, foreign and damaged streams.
+Through the drop-in symbols of src/snappy.h and through the batch API."""
+import random
+import struct
+
+import numpy as np
+import pytest
+
+from librdkafka_amd import workload as W
+from test_oracle_snappy import snappy_cases
+
+pytestmark = pytest.mark.gpu
+
+
+def _pack(items, align=64):
+    offs, pos = [], 0
+    for b in items:
+        offs.append(pos)
+        pos += (len(b) + align - 1) // align * align
+    buf = bytearray(pos + 256)
+    for o, b in zip(offs, items):
+        buf[o:o + len(b)] = b
+    return buf, offs
+
+
+def _compress_batch(engine, inputs):
+    import torch
+    hbuf, hoffs = _pack(inputs)
+    d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
+    in_offs = torch.tensor(hoffs, dtype=torch.int64, device="cuda")
+    in_lens = torch.tensor([len(b) for b in inputs], dtype=torch.int32, device="cuda")
+    bounds = [engine.snappy_max_compressed_length(len(b)) for b in inputs]
+    ooffs = np.concatenate([[0], np.cumsum([(b + 63) // 64 * 64 for b in bounds])[:-1]]).astype(np.int64)
+    d_out = torch.zeros(int(ooffs[-1]) + bounds[-1] + 256, dtype=torch.uint8, device="cuda")
+    out_offs = torch.tensor(ooffs, dtype=torch.int64, device="cuda")
+    out_lens = torch.zeros(len(inputs), dtype=torch.int32, device="cuda")
+    engine.snappy_compress_batch(d_in, in_offs, in_lens, d_out, out_offs, out_lens)
+    host = bytes(d_out.cpu().numpy())
+    fl = out_lens.cpu().numpy()
+    return [host[ooffs[i]:ooffs[i] + fl[i]] for i in range(len(inputs))]
+
+
+def _uncompress_batch(engine, streams, caps=None):
+    import torch
+    hbuf, hoffs = _pack(streams)
+    d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
+    in_offs = torch.tensor(hoffs, dtype=torch.int64, device="cuda")
+    in_lens = torch.tensor([len(b) for b in streams], dtype=torch.int32, device="cuda")
+    if caps is None:
+        caps = []
+        for s in streams:   # the reader sizes its buffer from the preamble
+            v, sh = 0, 0
+            for b in s[:5]:
+                v |= (b & 127) << sh
+                sh += 7
+                if b < 128:
+                    break
+            caps.append(min(v, 1 << 26))
+    ooffs = np.concatenate([[0], np.cumsum([(c + 255) // 64 * 64 for c in caps])[:-1]]).astype(np.int64)
+    d_out = torch.zeros(int(ooffs[-1]) + caps[-1] + 512, dtype=torch.uint8, device="cuda")
+    out_offs = torch.tensor(ooffs, dtype=torch.int64, device="cuda")
+    out_caps = torch.tensor(caps, dtype=torch.int32, device="cuda")
+    out_lens = torch.zeros(len(streams), dtype=torch.int32, device="cuda")
+    status = torch.full((len(streams),), 77, dtype=torch.int32, device="cuda")
+    engine.snappy_uncompress_batch(d_in, in_offs, in_lens, d_out, out_offs, out_caps, out_lens, status)
+    host = bytes(d_out.cpu().numpy())
+    st, ol = status.cpu().numpy(), out_lens.cpu().numpy()
+    return [(int(st[i]), host[ooffs[i]:ooffs[i] + ol[i]] if st[i] == 0 else b"") for i in range(len(streams))]
+
+
+def test_batch_compress_matches_oracle_and_an_independent_decoder(engine, oracle_mod):
+    pa = pytest.importorskip("pyarrow")
+    inputs = snappy_cases(seed=21, extra=40)
+    got = _compress_batch(engine, inputs)
+    for i, (d, c) in enumerate(zip(inputs, got)):
+        assert c == oracle_mod.snappy_compress(d), (i, len(d), len(c))
+        if d:
+            assert pa.decompress(c, decompressed_size=len(d), codec="snappy", asbytes=True) == d, i
+
+
+def test_dropin_compress_iov_segments(engine, oracle_mod):
+    rnd = random.Random(3)
+    data = W.gen_json(300001, 3)
+    cuts = sorted(rnd.sample(range(1, len(data)), 9))
+    segs = [data[a:b] for a, b in zip([0] + cuts, cuts + [len(data)])]
+    err, c = engine.rd_kafka_snappy_compress_iov(segs)
+    assert err == 0 and c == oracle_mod.snappy_compress(data)
+    for d in (b"", b"x", b"hello world" * 3, bytes(70000)):
+        assert engine.rd_kafka_snappy_compress_iov(d) == (0, oracle_mod.snappy_compress(d))
+
+
+def test_batch_uncompress_own_and_foreign_streams(engine, oracle_mod):
+    pa = pytest.importorskip("pyarrow")
+    inputs = snappy_cases(seed=22, extra=30)
+    own = [oracle_mod.snappy_compress(d) for d in inputs]
+    foreign = [pa.compress(d, codec="snappy", asbytes=True) if d else b"\x00" for d in inputs]
+    for streams in (own, foreign):
+        res = _uncompress_batch(engine, streams)
+        for i, (d, (st, out)) in enumerate(zip(inputs, res)):
+            assert st == 0 and out == d, (i, st, len(d), len(out))
+
+
+def test_uncompress_verdicts_on_damaged_streams(engine, oracle_mod):
+    rnd = random.Random(9)
+    base = [W.gen_json(5000, 4), bytes(3000) + W.gen_json(2000, 1), (rnd.randbytes(100) * 60)]
+    streams = []
+    for d in base:
+        c = oracle_mod.snappy_compress(d)
+        for _ in range(150):
+            m = bytearray(c)
+            k = rnd.randrange(4)
+            if k == 0:
+                m = m[:rnd.randrange(len(m))]
+            elif k == 1:
+                m += rnd.randbytes(rnd.randrange(1, 4))
+            else:
+                for _ in range(rnd.randrange(1, 4)):
+                    m[rnd.randrange(len(m))] = rnd.randrange(256)
+            streams.append(bytes(m))
+    # hand-made: every element form, and every way to fail
+    streams += [bytes([70]) + bytes([60 << 2, 69]) + bytes(range(70)),
+                bytes([8, 0]) + b"a" + bytes([1 | (3 << 2), 1]),
+                bytes([12, 3 << 2]) + b"abcd" + bytes([2 | (7 << 2), 4, 0]),
+                bytes([12, 3 << 2]) + b"abcd" + bytes([3 | (7 << 2), 4, 0, 0, 0]),
+                bytes([8, 0]) + b"a" + bytes([1 | (3 << 2), 0]),
+                bytes([8, 0]) + b"a" + bytes([1 | (3 << 2), 2]),
+                bytes([8, 0]) + b"a" + bytes([1 | (3 << 2)]),
+                bytes([9, 0]) + b"a" + bytes([1 | (3 << 2), 1]),
+                bytes([7, 0]) + b"a" + bytes([1 | (3 << 2), 1]),
+                bytes([2, 1 << 2]) + b"a", bytes([0]), bytes([0, 0, 0x61])]
+    caps = []
+    want = []
+    for s in streams:
+        n = oracle_mod.snappy_uncompressed_length(s)
+        caps.append(min(n, 1 << 24) if n is not None else 0)
+        err, out = oracle_mod.snappy_uncompress(s)
+        want.append((err, out))
+    keep = [i for i, s in enumerate(streams) if len(s) and caps[i] <= (1 << 23)]
+    res = _uncompress_batch(engine, [streams[i] for i in keep], [caps[i] for i in keep])
+    bad = 0
+    for j, i in enumerate(keep):
+        st, out = res[j]
+        err, exp = want[i]
+        assert (st == 0) == (err == 0), (i, streams[i][:40].hex(), st, err)
+        if err == 0:
+            assert out == exp, i
+        else:
+            assert st == engine.SNAPPY_E_IO, (i, st)
+            bad += 1
+    assert bad > 100
+
+
+def test_dropin_reader_case_bare_and_snappy_java(engine, oracle_mod):
+    a, b, c3 = W.gen_json(70000, 1), W.gen_json(123, 2), W.gen_json(40000, 3)
+    ca, cb, cc = (oracle_mod.snappy_compress(x) for x in (a, b, c3))
+    assert engine.rd_kafka_snappy_decompress(ca) == (0, a)
+    hdr = b"\x82SNAPPY\x00" + struct.pack(">II", 1, 1)
+    framed = hdr + b"".join(struct.pack(">I", len(x)) + x for x in (ca, cb, cc))
+    assert engine.rd_kafka_snappy_decompress(framed) == (0, a + b + c3)
+    for damaged in (framed + b"\x00", framed[:-1], hdr + struct.pack(">I", 1) + b"\x00",
+                    b"\xff\xff\xff\xff\xff", framed[:40] + b"\x00" + framed[41:]):
+        got = engine.rd_kafka_snappy_decompress(damaged)
+        assert got == oracle_mod.rdk_snappy_decompress(damaged), damaged[:24].hex()
+
+
+def test_roundtrip_at_scale(engine):
+    """64 x 1 MiB JSON through compress -> uncompress on the device (property check at the
+    bench's size; the oracle comparison above covers the bytes)."""
+    import torch
+    n = 64
+    src, offs, lens = (None, None, None)
+    data = [W.gen_json(1 << 20, 100 + i) for i in range(4)]
+    inputs = [data[i % 4] for i in range(n)]
+    streams = _compress_batch(engine, inputs)
+    res = _uncompress_batch(engine, streams)
+    for i in range(n):
+        assert res[i] == (0, inputs[i]), i
+    assert torch.cuda.is_available()

@@ -308,6 +308,76 @@ def bench_lz4c(args, rank, world, n=None, fast=False, level=0):
             "frames": (dst, ooffs, olens)}
 
 
+def bench_snappy(args, rank, world, n=None, decompress=False):
+    """snappy (compression.codec=snappy) on 1 MiB JSON batches: the codec behind
+    rd_kafka_msgset_writer_compress_snappy (rdkafka_msgset_writer.c:1041) or the reader's
+    snappy case (rdkafka_msgset_reader.c:299-390).  Streams are the reference's
+    compress_fragment parse; the decompress leg decodes them and compares."""
+    import torch
+    import librdkafka_amd as L
+    n = n or args.partitions
+    src, offs, lens = json_batches(n, seed=42 + rank)
+    bound = (L.snappy_max_compressed_length(JSON_BATCH) + 255) // 256 * 256
+    dst = torch.empty(n * bound + 256, dtype=torch.uint8, device="cuda")
+    ooffs = torch.arange(n, dtype=torch.int64, device="cuda") * bound
+    olens = torch.zeros(n, dtype=torch.int32, device="cuda")
+    comp = lambda: L.snappy_compress_batch(src, offs, lens, dst, ooffs, olens)  # noqa: E731
+    if not decompress:
+        ms, kms = _timed(comp, args.steps, args.warmup, world)
+        clen = int(olens.sum())
+        return {"ms": ms, "kernel_ms": kms, "bytes": n * JSON_BATCH, "records": n,
+                "alg_bytes": n * JSON_BATCH + clen, "ratio": n * JSON_BATCH / clen}
+    comp()
+    clen = int(olens.sum())
+    out = torch.empty(n * JSON_BATCH + 256, dtype=torch.uint8, device="cuda")
+    caps = torch.full((n,), JSON_BATCH, dtype=torch.int32, device="cuda")
+    dlens = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ms, kms = _timed(lambda: L.snappy_uncompress_batch(dst, ooffs, olens, out, offs, caps, dlens, st),
+                     args.steps, args.warmup, world)
+    assert int(st.abs().sum()) == 0 and torch.equal(out[:n * JSON_BATCH], src[:n * JSON_BATCH])
+    return {"ms": ms, "kernel_ms": kms, "bytes": n * JSON_BATCH, "records": n,
+            "alg_bytes": n * JSON_BATCH + clen}
+
+
+def cpu_baseline_snappy(kind, n=64, seconds=4.0):
+    """The oracle's restatement of snappy.c (snappy.c itself needs the generated config.h)
+    on CPU_THREADS host threads over n x 1 MiB JSON batches."""
+    import numpy as np
+    import oracle
+    import librdkafka_amd as L
+    lib = oracle.lib()
+    data = np.frombuffer(L.gen_json(JSON_BATCH * 8, 42), dtype=np.uint8)
+    src = np.concatenate([data] * (n // 8))
+    offs = (np.arange(n, dtype=np.uint64) * JSON_BATCH).astype(np.uint64)
+    lens = np.full(n, JSON_BATCH, dtype=np.uint32)
+    bound = int(lib.or_snappy_max_compressed_length(JSON_BATCH))
+    cbuf = np.zeros(n * bound, dtype=np.uint8)
+    coffs = (np.arange(n, dtype=np.uint64) * bound).astype(np.uint64)
+    clens = np.zeros(n, dtype=np.uint32)
+    comp = lambda: lib.or_snappy_batches_mt(  # noqa: E731
+        src.ctypes.data, offs.ctypes.data, lens.ctypes.data, n, cbuf.ctypes.data,
+        coffs.ctypes.data, clens.ctypes.data, 0, CPU_THREADS)
+    assert comp() == 0
+    dbuf = np.zeros(n * JSON_BATCH, dtype=np.uint8)
+    dlens = np.zeros(n, dtype=np.uint32)
+    dec = lambda: lib.or_snappy_batches_mt(  # noqa: E731
+        cbuf.ctypes.data, coffs.ctypes.data, clens.ctypes.data, n, dbuf.ctypes.data,
+        offs.ctypes.data, dlens.ctypes.data, 1, CPU_THREADS)
+    fn = comp if kind == "compress" else dec
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        assert fn() == 0
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(passes * n * JSON_BATCH / el / 1e9, 3), "unit": "GB/s",
+            "cores": CPU_THREADS, "kind": "port",
+            "sample": f"{n} x 1 MiB JSON batches, {passes} passes, snappy.c's "
+                      f"{'compress_fragment' if kind == 'compress' else 'decoder'} restated, {cpu_model()}"}
+
+
 def bench_consumer(args, rank, world, n=None):
     """configs[3]: consumer path per fetched v2 batch: CRC32C verify
     (check.crcs, rdkafka_msgset_reader.c:982-1015) then LZ4F decompress
@@ -911,7 +981,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="finalize",
                     choices=["finalize", "finalize_fast", "crc", "lz4c", "lz4c_fast", "lz4hc",
-                             "consumer", "producer", "serialize", "index", "legacy"])
+                             "consumer", "producer", "serialize", "index", "legacy", "snappyc",
+                             "snappyd"])
     ap.add_argument("--batches", type=int, default=CRC_BATCHES, help="--workload crc: batches per GPU")
     ap.add_argument("--partitions", type=int, default=512,
                     help="toppars (1 MiB batches) per GPU")
@@ -970,6 +1041,9 @@ def main():
             res = bench_index(args, rank, world, n=args.partitions)
         elif args.workload == "legacy":
             res = bench_legacy(args, rank, world, n=args.partitions)
+        elif args.workload.startswith("snappy"):
+            res = bench_snappy(args, rank, world, n=args.partitions,
+                               decompress=args.workload == "snappyd")
         else:
             res = bench_consumer(args, rank, world, n=args.partitions)
         t_max = max_over_ranks(res["ms"], world)
@@ -982,6 +1056,8 @@ def main():
                     cpu = cpu_baseline_index(*res["host_sample"])
                 elif args.workload == "legacy":
                     cpu = cpu_baseline_legacy(*res["host_sample"])
+                elif args.workload.startswith("snappy"):
+                    cpu = cpu_baseline_snappy("compress" if args.workload == "snappyc" else "decompress")
                 else:
                     cpu = cpu_reference_lz4("decompress" if args.workload == "consumer"
                                             else "compress",
@@ -1079,6 +1155,14 @@ def main():
                 "lz4hc_compress_level12_1MiB_json",
                 bench_lz4c(argparse.Namespace(steps=2, warmup=1, partitions=256), rank, world, n=256,
                            level=12), 2, 1, cpu("compress", level=12))
+            legs["snappy_compress_1MiB_json"] = leg_line(
+                "snappy_compress_1MiB_json", bench_snappy(sub, rank, world, n=256), 3, 1,
+                None if no_cpu else cpu_baseline_snappy("compress"))
+            legs["snappy_uncompress_1MiB_json"] = leg_line(
+                "snappy_uncompress_1MiB_json",
+                bench_snappy(argparse.Namespace(steps=3, warmup=1, partitions=1024), rank, world,
+                             n=1024, decompress=True), 3, 1,
+                None if no_cpu else cpu_baseline_snappy("decompress"))
             legs["consumer_crc_verify_lz4f_decompress_1MiB"] = leg_line(
                 "consumer_crc_verify_lz4f_decompress_1MiB",
                 bench_consumer(argparse.Namespace(steps=3, warmup=1, partitions=1024), rank, world,
@@ -1103,6 +1187,7 @@ LEG_NAMES = {"lz4c": "lz4f_compress_1MiB_json", "lz4c_fast": "lz4f_compress_fast
              "consumer": "consumer_crc_verify_lz4f_decompress_1MiB",
              "serialize": "v2_record_serialize_1MiB_json", "index": "v2_record_index_1MiB_json",
              "legacy": "v1_msgset_crc32_verify_1MiB_json",
+             "snappyc": "snappy_compress_1MiB_json", "snappyd": "snappy_uncompress_1MiB_json",
              "producer": "producer_pipeline_1MiB_json_pcie"}
 
 

@@ -65,6 +65,9 @@ def lib():
         L.or_snappy_uncompressed_length.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
         L.or_snappy_uncompress.restype = C.c_int
         L.or_snappy_uncompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+        L.or_snappy_batches_mt.restype = C.c_int
+        L.or_snappy_batches_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         L.or_rdk_snappy_decompress.restype = C.c_int
         L.or_rdk_snappy_decompress.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p),
                                                C.POINTER(C.c_size_t)]

@@ -153,6 +153,10 @@ int or_snappy_uncompress(const uint8_t *p, size_t n, uint8_t *out);
 /* the reader's snappy case (rdkafka_msgset_reader.c:299-390), snappy-java framing
  * included: 0 and a malloc()ed payload (or_free), or an OR_ERR_ code */
 int or_rdk_snappy_decompress(const uint8_t *in, size_t inlen, uint8_t **out, size_t *outlen);
+/* threaded batch driver for the timed CPU baseline: dec = 0 compress, 1 uncompress */
+int or_snappy_batches_mt(const uint8_t *base, const uint64_t *offs, const uint32_t *lens, size_t n,
+                         uint8_t *out, const uint64_t *out_offs, uint32_t *out_lens, int dec,
+                         int threads);
 
 #ifdef __cplusplus
 }

@@ -93,7 +93,17 @@ static uint8_t *sn_compress_fragment(const uint8_t *in, size_t n, uint8_t *op, u
             do {                                   /* :1054-1088 */
                 const uint8_t *base = ip, *s1 = cand + 4, *s2 = ip + 4;
                 int matched = 4;
-                while (s2 < ip_end && *s1 == *s2) { s1++; s2++; matched++; }   /* find_match_length */
+                /* find_match_length (:823-866): 8 bytes at a time, then the tail */
+                while (s2 + 8 <= ip_end) {
+                    uint64_t a, b;
+                    memcpy(&a, s1, 8);
+                    memcpy(&b, s2, 8);
+                    if (a == b) { s1 += 8; s2 += 8; matched += 8; continue; }
+                    matched += __builtin_ctzll(a ^ b) >> 3;
+                    goto counted;
+                }
+                while (s2 < ip_end && *s1 == *s2) { s1++; s2++; matched++; }
+            counted:
                 ip += matched;
                 op = sn_emit_copy(op, (int)(base - cand), matched);
                 next_emit = ip;
@@ -186,7 +196,11 @@ int or_snappy_uncompress(const uint8_t *p, size_t n, uint8_t *out) {
             const uint32_t off = kind == 1 ? ((uint32_t)(c >> 5) << 8) | trailer : trailer;
             if ((uint32_t)op <= off - 1u) return SN_EIO;   /* writer_append_from_self (:543) */
             if (ulen - op < len) return SN_EIO;
-            for (uint32_t i = 0; i < len; i++) out[op + i] = out[op + i - off];
+            if (off >= len) {                      /* no overlap: one block copy */
+                memcpy(out + op, out + op - off, len);
+            } else {                               /* incremental_copy (:484): the pattern repeats */
+                for (uint32_t i = 0; i < len; i++) out[op + i] = out[op + i - off];
+            }
             op += len;
         }
     }
@@ -239,4 +253,54 @@ int or_rdk_snappy_decompress(const uint8_t *in, size_t inlen, uint8_t **out, siz
     *out = buf;
     *outlen = ulen;
     return 0;
+}
+
+/* ---- threaded drivers (bench.py's cpu_baseline leg) ----------------------- */
+#include <pthread.h>
+
+struct sn_job {
+    const uint8_t *base; const uint64_t *offs; const uint32_t *lens; size_t lo, hi;
+    uint8_t *out; const uint64_t *out_offs; uint32_t *out_lens; int dec; int rc;
+};
+
+static void *sn_worker(void *arg) {
+    struct sn_job *j = (struct sn_job *)arg;
+    for (size_t i = j->lo; i < j->hi; i++) {
+        if (j->dec) {
+            size_t ulen;
+            if (!or_snappy_uncompressed_length(j->base + j->offs[i], j->lens[i], &ulen) ||
+                or_snappy_uncompress(j->base + j->offs[i], j->lens[i], j->out + j->out_offs[i])) {
+                j->rc = SN_EIO;
+                continue;
+            }
+            j->out_lens[i] = (uint32_t)ulen;
+        } else {
+            size_t clen;
+            if (or_snappy_compress(j->base + j->offs[i], j->lens[i], j->out + j->out_offs[i], &clen)) {
+                j->rc = -12;
+                continue;
+            }
+            j->out_lens[i] = (uint32_t)clen;
+        }
+    }
+    return NULL;
+}
+
+/* n inputs -> n streams (dec = 0) or n streams -> n payloads (dec = 1) on `threads` threads;
+ * every output slot holds the bound / the declared length */
+int or_snappy_batches_mt(const uint8_t *base, const uint64_t *offs, const uint32_t *lens, size_t n,
+                         uint8_t *out, const uint64_t *out_offs, uint32_t *out_lens, int dec,
+                         int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 512) threads = 512;
+    pthread_t th[512];
+    struct sn_job jobs[512];
+    int rc = 0;
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (struct sn_job){base, offs, lens, n * t / threads, n * (t + 1) / threads,
+                                  out, out_offs, out_lens, dec, 0};
+        pthread_create(&th[t], NULL, sn_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) { pthread_join(th[t], NULL); if (jobs[t].rc) rc = jobs[t].rc; }
+    return rc;
 }

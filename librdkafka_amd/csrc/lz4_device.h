@@ -32,7 +32,9 @@ __device__ __forceinline__ uint32_t ld32u(uintptr_t a) {
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+// lane mask of a predicate, straight from the compare (HIP's __ballot takes an int and
+// costs a 0/1 round trip through a VGPR)
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 __device__ __forceinline__ int ffs64(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
 

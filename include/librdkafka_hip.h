@@ -296,6 +296,7 @@ typedef struct rdk_hip_batch_s {
 } rdk_hip_batch_t;
 #define RDK_HIP_PRODUCER_EXACT 0 /* frames byte-identical to rd_kafka_lz4_compress */
 #define RDK_HIP_PRODUCER_FAST 1  /* rdk_hip_lz4f_compress_fast frames */
+#define RDK_HIP_PRODUCER_SNAPPY 2 /* compression.codec=snappy: rdk_hip_snappy_compress streams */
 #define RDK_HIP_E_BUSY (-5)      /* every slot is in flight: poll() first */
 /* The writer's finalize (rd_kafka_msgset_writer_finalize, rdkafka_msgset_writer.c:1335:
  * rd_kafka_msgset_writer_compress :1128-1221 -> finalize_MessageSet_v2_header :1251-1295
@@ -307,7 +308,9 @@ typedef struct rdk_hip_batch_s {
  * and the LZ4 codec bits set, the LZ4F frame (or the plain records when the frame would
  * be larger, :1179), CRC32C stored at offset 17.  d_frame_lens[i] = frame size,
  * d_batch_lens[i] = 12 + Length, d_crcs[i] = the CRC.  mode is RDK_HIP_PRODUCER_EXACT
- * (frames byte-identical to rd_kafka_lz4_compress at level 0) or _FAST.  This is what
+ * (frames byte-identical to rd_kafka_lz4_compress at level 0), _FAST, or _SNAPPY (the
+ * payload is the snappy stream of rd_kafka_snappy_compress_iov, the codec bits are 2 and
+ * the slot capacity is 61 + rdk_hip_snappy_max_compressed_length(len)).  This is what
  * the producer front-end runs per staging slot. */
 int rdk_hip_msgset_v2_finalize(const void *d_in, const uint64_t *d_rec_offs,
                                const uint32_t *d_rec_lens, void *d_out,

@@ -480,7 +480,7 @@ def lz4f_decompress_batch_noalloc(src, in_offs, in_lens, dst, out_offs, out_caps
            "lz4f_decompress_noalloc")
 
 
-PRODUCER_EXACT, PRODUCER_FAST = 0, 1
+PRODUCER_EXACT, PRODUCER_FAST, PRODUCER_SNAPPY = 0, 1, 2
 E_BUSY = -5
 
 

@@ -55,6 +55,10 @@ struct Slot {
 }  // namespace
 
 size_t lz4f_compress_bound(size_t len);
+size_t snappy_max_compressed_length(size_t len);
+int snappy_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
+                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                           uint32_t n, hipStream_t s);
 int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
                          const uint32_t *d_in_lens, uint8_t *d_out, const uint64_t *d_out_offs,
                          uint32_t *d_out_lens, uint32_t n, int accel, hipStream_t s,
@@ -104,7 +108,48 @@ Meta meta_at(uint8_t *base, uint32_t B) {
 }
 size_t meta_bytes(uint32_t B) { return size_t(B) * (4 * 8 + 5 * 4) + 16; }
 
-size_t out_span(size_t len) { return (kV2Hdr + lz4f_compress_bound(len) + 255) & ~size_t(255); }
+size_t out_span(size_t len, int mode) {
+  const size_t bound = mode == RDK_HIP_PRODUCER_SNAPPY ? snappy_max_compressed_length(len)
+                                                       : lz4f_compress_bound(len);
+  return (kV2Hdr + bound + 255) & ~size_t(255);
+}
+
+// compression.codec=snappy: the writer's codec choice and header for batch i, whose snappy
+// stream (d_frame_lens[i] bytes) sits 61 bytes into its output slot.  A stream larger than
+// the records is thrown away (rdkafka_msgset_writer.c:1179), else Attributes |= SNAPPY
+// (:1187); Length = size - 12 (:1265).  The CRC32C pass follows.  One workgroup per batch.
+__global__ __launch_bounds__(256) void snappy_v2_header_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ rec_offs,
+    const uint32_t *__restrict__ rec_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
+    const uint32_t *__restrict__ frame_lens, uint32_t *__restrict__ batch_lens, uint32_t n) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t len = rec_lens[i], clen = frame_lens[i];
+    const uint8_t *rec = in + rec_offs[i];
+    uint8_t *ob = out + out_offs[i];
+    const bool compressed = clen <= len;
+    const uint32_t payload = compressed ? clen : len;
+    if (!compressed)
+      for (uint32_t k = t; k < len; k += 256u) ob[kV2Hdr + k] = rec[k];
+    if (t < kV2Hdr) {
+      uint32_t v = rec[int(t) - int(kV2Hdr)];
+      const uint32_t length = kV2Hdr + payload - 12u;
+      if (t >= 8 && t < 12) v = (length >> (8u * (3u - (t - 8u)))) & 0xFFu;
+      if (t == 22 && compressed) v |= 2u;  // RD_KAFKA_COMPRESSION_SNAPPY
+      ob[t] = uint8_t(v);
+    }
+    if (t == 0) batch_lens[i] = kV2Hdr + payload;
+  }
+}
+
+// d_crcs[i] = the CRC stored big-endian at offset 17 of batch i
+__global__ void v2_crc_gather_kernel(const uint8_t *__restrict__ out, const uint64_t *__restrict__ out_offs,
+                                     uint32_t *__restrict__ crcs, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *p = out + out_offs[i] + 17;
+  crcs[i] = (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3];
+}
 
 // Finished batches -> the slot's pinned host buffer, packed back to back (16-byte aligned,
 // in completion order of an atomic cursor) by the GPU itself: only the batches' own bytes
@@ -143,12 +188,32 @@ RDK_API int rdk_hip_msgset_v2_finalize(const void *d_in, const uint64_t *d_rec_o
   if (!d_in || !d_rec_offs || !d_rec_lens || !d_out || !d_out_offs || !d_out_caps ||
       !d_frame_lens || !d_batch_lens || !d_crcs)
     return set_error(RDK_HIP_E_INVAL, "null pointer");
-  if (mode != RDK_HIP_PRODUCER_EXACT && mode != RDK_HIP_PRODUCER_FAST)
+  if (mode != RDK_HIP_PRODUCER_EXACT && mode != RDK_HIP_PRODUCER_FAST &&
+      mode != RDK_HIP_PRODUCER_SNAPPY)
     return set_error(RDK_HIP_E_INVAL, "bad mode %d", mode);
   hipStream_t s = static_cast<hipStream_t>(stream);
   Ctx *c = ctx();
   if (!c) return RDK_HIP_E_NODEV;
-  (void)d_out_caps;  // slots are sized by the caller from rdk_hip_lz4f_compress_bound()
+  if (mode == RDK_HIP_PRODUCER_SNAPPY) {
+    // snappy: fragments + assembly, then the codec choice and header, then the CRC32C pass
+    // over the finished batches (the CRC is not fused into this compressor)
+    uint8_t *ob = static_cast<uint8_t *>(d_out);
+    int rc = snappy_compress_device(static_cast<const uint8_t *>(d_in), d_rec_offs, d_rec_lens,
+                                    ob + kV2Hdr, d_out_offs, d_frame_lens, n, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(snappy_v2_header_kernel, dim3(n < 4096u ? n : 4096u), dim3(256), 0, s,
+                       static_cast<const uint8_t *>(d_in), d_rec_offs, d_rec_lens, ob, d_out_offs,
+                       d_frame_lens, d_batch_lens, n);
+    RDK_HIP_CHECK(hipGetLastError());
+    // d_crcs doubles as the CRC pass's status array, then takes the CRC values
+    rc = rdk_hip_msgset_v2_crc(d_out, d_out_offs, d_out_caps, d_crcs, n, RDK_HIP_V2_CRC_FINALIZE, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(v2_crc_gather_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, ob, d_out_offs,
+                       d_crcs, n);
+    RDK_HIP_CHECK(hipGetLastError());
+    return RDK_HIP_OK;
+  }
+  (void)d_out_caps;  // slots are sized by the caller from the codec's bound
   // Two launches: the block kernel, which also leaves the raw CRC32C register of every
   // block it writes (crc_wave.h), and the frame assembler, which also makes the writer's
   // codec choice, finishes the header and combines the batch's CRC from those registers.
@@ -215,7 +280,9 @@ void release(rdk_hip_producer_s *p) {
 RDK_API rdk_hip_producer_t *rdk_hip_producer_new(int device, size_t slot_bytes, int nslots,
                                                   int mode) {
   if (rdk_hip_init(device)) return nullptr;
-  if (nslots < 1 || slot_bytes < 4096 || (mode != RDK_HIP_PRODUCER_EXACT && mode != RDK_HIP_PRODUCER_FAST)) {
+  if (nslots < 1 || slot_bytes < 4096 ||
+      (mode != RDK_HIP_PRODUCER_EXACT && mode != RDK_HIP_PRODUCER_FAST &&
+       mode != RDK_HIP_PRODUCER_SNAPPY)) {
     set_error(RDK_HIP_E_INVAL, "producer: bad arguments");
     return nullptr;
   }
@@ -226,7 +293,7 @@ RDK_API rdk_hip_producer_t *rdk_hip_producer_new(int device, size_t slot_bytes, 
   p->slot_bytes = slot_bytes;
   p->max_batches = uint32_t(slot_bytes / 512 + 64);
   // worst case: every batch at most slot_bytes, spans rounded up
-  p->out_bytes = out_span(slot_bytes) + size_t(p->max_batches) * 512;
+  p->out_bytes = out_span(slot_bytes, mode) + size_t(p->max_batches) * 512;
   p->slots.resize(size_t(nslots));
   const size_t mb = meta_bytes(p->max_batches);
   for (Slot &sl : p->slots) {
@@ -253,7 +320,7 @@ RDK_API int rdk_hip_producer_produce(rdk_hip_producer_t *p, const void *hdr61, c
                                      uint32_t len, uint64_t cookie) {
   if (!p || !hdr61 || (!records && len)) return set_error(RDK_HIP_E_INVAL, "null pointer");
   const size_t need_in = (kV2Hdr + size_t(len) + 64 + 15) & ~size_t(15);
-  const size_t need_out = out_span(len);
+  const size_t need_out = out_span(len, p->mode);
   if (need_in > p->slot_bytes || need_out > p->out_bytes)
     return set_error(RDK_HIP_E_INVAL, "batch of %u bytes exceeds the slot", len);
   Slot *sl = &p->slots[size_t(p->fill)];

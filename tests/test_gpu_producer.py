@@ -21,6 +21,16 @@ def _check_batch(oracle_mod, hdr, records, out, crc, mode_exact):
     assert int.from_bytes(out[17:21], "big") == crc == oracle_mod.crc32c(0, out[21:])
     attr = int.from_bytes(out[21:23], "big")
     payload = out[61:]
+    if mode_exact == "snappy":                                                # codec bits 2
+        ref = oracle_mod.snappy_compress(records)
+        if attr & 7 == 2:
+            assert attr == int.from_bytes(hdr[21:23], "big") | 2
+            assert payload == ref and len(payload) <= len(records)
+            assert oracle_mod.snappy_uncompress(payload) == (0, records)
+        else:
+            assert attr == int.from_bytes(hdr[21:23], "big")
+            assert payload == records and len(ref) > len(records)
+        return
     ref_err, ref_frame = oracle_mod.rdk_lz4_compress(records)
     if attr & 7 == 3:                                                         # LZ4
         assert attr == int.from_bytes(hdr[21:23], "big") | 3
@@ -36,7 +46,7 @@ def _check_batch(oracle_mod, hdr, records, out, crc, mode_exact):
             assert len(ref_frame) > len(records)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 def test_producer_batches(engine, oracle_mod, mode):
     rnd = random.Random(50 + mode)
     p = engine.Producer(0, slot_bytes=4 << 20, nslots=3, mode=mode)
@@ -62,7 +72,7 @@ def test_producer_batches(engine, oracle_mod, mode):
     assert sorted(got) == sorted(sent)
     for i, (hdr, rec) in sent.items():
         out, crc = got[i]
-        _check_batch(oracle_mod, hdr, rec, out, crc, mode == 0)
+        _check_batch(oracle_mod, hdr, rec, out, crc, "snappy" if mode == 2 else mode == 0)
 
 
 def test_producer_order_and_busy(engine):
@@ -86,7 +96,7 @@ def test_producer_order_and_busy(engine):
     p.close()
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 def test_msgset_v2_finalize_device_batches(engine, oracle_mod, mode):
     """rdk_hip_msgset_v2_finalize on device-resident MessageSets (the writer's compress +
     header finalize + CRC32C in one call): every finished batch checked field by field
@@ -110,7 +120,8 @@ def test_msgset_v2_finalize_device_batches(engine, oracle_mod, mode):
     for o, (hdr, rec) in zip(in_offs, items):
         hbuf[o - 61:o] = hdr
         hbuf[o:o + len(rec)] = rec
-    caps = [(61 + engine.lz4f_compress_bound(len(rec)) + 255) // 256 * 256 for _, rec in items]
+    bound = engine.snappy_max_compressed_length if mode == 2 else engine.lz4f_compress_bound
+    caps = [(61 + bound(len(rec)) + 255) // 256 * 256 for _, rec in items]
     out_offs = np.concatenate([[0], np.cumsum(caps)[:-1]])
     n = len(items)
     d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
@@ -125,4 +136,4 @@ def test_msgset_v2_finalize_device_batches(engine, oracle_mod, mode):
     cr = crcs.cpu().numpy().view(np.uint32)
     for i, (hdr, rec) in enumerate(items):
         out = host[out_offs[i]:out_offs[i] + bl[i]]
-        _check_batch(oracle_mod, hdr, rec, out, int(cr[i]), mode == 0)
+        _check_batch(oracle_mod, hdr, rec, out, int(cr[i]), "snappy" if mode == 2 else mode == 0)

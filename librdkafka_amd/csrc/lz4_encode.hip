@@ -50,6 +50,7 @@
 #include "lz4_device.h"
 #include "lz4_engine.h"
 #include "lz4_wave.h"
+#include "win_ring.h"
 
 namespace rdk {
 
@@ -327,88 +328,15 @@ constexpr uint32_t kShortLit = 16;  // literal runs copied by their own lane
 enum WinMode { W_SEARCH = 0, W_POSTMATCH = 1, W_FORCED = 2 };
 enum WinStatus { W_CONTINUE = 0, W_LAST = 1, W_OVERFLOW = 2 };
 
-struct WinBlock {
-  uintptr_t src, dst;
-  rsrc_t r;   // the block's dwords (reads outside return 0)
+struct WinBlock : SrcRing {  // + the block's source and its LDS ring (win_ring.h)
+  uintptr_t dst;
   rsrc_t w;   // the block's output slot (byte stores; parked lanes write nothing)
-  uint32_t sa;  // src & 3: byte offset of position 0 inside the read resource
   int n, mfl1, mlim, olimit;  // size, mflimitPlusOne, matchlimit, dstCapacity
   int ip;      // next probe (W_SEARCH) / end of the last match (W_POSTMATCH)
   int cnt;     // probes already made in the current search
   int anchor, op;
   int mode;    // how the next window starts
-  // source ring in LDS: virtual positions (position + sa) [H - kRingBytes, H) are at
-  // ring[v & (kRingBytes-1)].  `pend` is the chunk at H, loaded one fill ahead.
-  lds_u32 *ring;
-  int H;
-  u32x4 pend;
 };
-
-constexpr uint32_t kRingBytes = 4096, kRingChunk = 1024;
-
-// ring[H, H+1 KiB) <- pend; the load of the following chunk is issued at once
-__device__ __forceinline__ void ring_fill(WinBlock &b, int lane) {
-  typedef __attribute__((address_space(3))) u32x4 lds_u4v;
-  const uint32_t at = (uint32_t(b.H) & (kRingBytes - 1u)) + 16u * uint32_t(lane);
-  *(lds_u4v *)((lds_u8 *)b.ring + at) = b.pend;
-  b.H += int(kRingChunk);
-  b.pend = __builtin_amdgcn_raw_buffer_load_b128(b.r, uint32_t(b.H) + 16u * uint32_t(lane), 0, 0);
-  asm volatile("" ::: "memory");
-}
-
-// nine dwords around virtual position v (4-aligned a = v & ~3): a-4 .. a+28, from the ring.
-// Eight consecutive dwords from the ring index of a; the few lanes whose window runs over
-// the end of the ring read again with every index wrapped (the straight reads past the
-// end land in the hash table behind the ring: harmless).
-__device__ __forceinline__ void ring_load9(const WinBlock &b, uint32_t a, uint32_t d[9]) {
-  const uint32_t at = a & (kRingBytes - 1u);
-  d[0] = *(lds_u32 *)((lds_u8 *)b.ring + ((a - 4u) & (kRingBytes - 1u)));
-  lds_u32 *p = (lds_u32 *)((lds_u8 *)b.ring + at);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) d[k + 1] = p[k];
-  const bool wraps = at > kRingBytes - 32u;
-  if (ballot(wraps)) {
-#pragma unroll
-    for (int k = 1; k < 8; ++k) {
-      const uint32_t v = *(lds_u32 *)((lds_u8 *)b.ring + ((at + 4u * uint32_t(k)) & (kRingBytes - 1u)));
-      if (wraps) d[k + 1] = v;
-    }
-  }
-}
-
-__device__ __forceinline__ bool ring_has(const WinBlock &b, int v_lo, int v_hi) {  // [v_lo, v_hi)
-  return v_lo >= b.H - int(kRingBytes) && v_hi <= b.H;
-}
-
-// equal bytes a[i]==b[i], i < limit, 64 per wave step; a / c are block positions.  Steps
-// whose bytes are all in the ring read LDS, the others global memory.
-__device__ __forceinline__ int win_count_fwd(const WinBlock &b, int a, int c, int limit, int lane) {
-  int cnt = 0;
-  while (cnt < limit) {
-    const int l = cnt + lane;
-    const int va = a + cnt + int(b.sa), vc = c + cnt + int(b.sa);
-    uint32_t x, y;
-    if (ring_has(b, vc, vc + 64) && ring_has(b, va, va + 64)) {
-      x = ((lds_u8 *)b.ring)[uint32_t(va + lane) & (kRingBytes - 1u)];
-      y = ((lds_u8 *)b.ring)[uint32_t(vc + lane) & (kRingBytes - 1u)];
-    } else {
-      x = l < limit ? ldb(b.src + uint32_t(a + l)) : 0u;
-      y = l < limit ? ldb(b.src + uint32_t(c + l)) : 1u;
-    }
-    const uint64_t m = ballot(l < limit && x == y);
-    const int run = m == ~0ull ? 64 : __builtin_ctzll(~m);
-    cnt += run;
-    if (run < 64) break;
-  }
-  return cnt;
-}
-
-__device__ __forceinline__ uint64_t bits_below(int x) {  // lanes [0, x), x in 0..64
-  return x >= 64 ? ~0ull : ((1ull << x) - 1ull);
-}
-__device__ __forceinline__ uint64_t bits_range(int a, int b) {  // lanes [a, b)
-  return a >= b ? 0ull : (bits_below(b) & ~bits_below(a));
-}
 
 // One window of 64 positions from w0.  See the file comment; tests/sim/lz4_window_sim.cpp
 // is the same walk with the lanes as arrays.
@@ -810,12 +738,9 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
 __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, lds_u32 *ring,
                             int lane) {
   WinBlock b;
-  b.src = src;
+  ring_init(b, src, uint32_t(n), ring, lane);
   b.dst = dst;
-  const uintptr_t lo = src & ~uintptr_t(3);
-  b.r = block_rsrc(lo, (src + uint32_t(n) + 3u) & ~uintptr_t(3));
   b.w = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(dst), 0, n, 0x00020000);
-  b.sa = uint32_t(src & 3u);
   b.n = n;
   b.mfl1 = n - kLz4MFLimit + 1;
   b.mlim = n - kLz4LastLiterals;
@@ -825,9 +750,6 @@ __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table,
   b.anchor = 0;
   b.op = 0;
   b.mode = W_SEARCH;
-  b.ring = ring;
-  b.H = 0;
-  b.pend = __builtin_amdgcn_raw_buffer_load_b128(b.r, 16u * uint32_t(lane), 0, 0);
   int forced = 0;
   for (;;) {
     int w0;

@@ -39,8 +39,12 @@
 // does not match the preamble), so the verdict is the reference's: 0 or -EIO.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "lz4_device.h"
+#include "lz4_wave.h"
+#include "win_ring.h"
 
 namespace rdk {
 
@@ -230,13 +234,522 @@ __device__ uint32_t sn_compress_fragment(uintptr_t src, uint32_t n, uintptr_t ds
   return op;
 }
 
+// ===================================================================== windows
+// compress_fragment in WINDOWS of 64 consecutive positions, one per lane (the scheme of the
+// exact LZ4 engine, lz4_encode.hip).  Every lane loads its own 36 source bytes and its table
+// candidate's 36 bytes once (from the LDS source ring, or from memory for candidates further
+// back than the ring), verifies the 4-byte match and measures it (28 bytes from registers,
+// up to 92 from the ring).  The sequential loop's path over those per-lane results -- which
+// positions are probed and inserted, the first verifying probe, the ip-1 insertion and the
+// immediate re-test behind a copy (:1071-1088) -- is the orbit of the entry lane under
+// next(m) = first verified lane >= m + len(m), found by pointer doubling (the parallel
+// walk).  The skip schedule leaves stride 1 after probe 31 of a search (skip++ >> 5 from
+// 32, :1019): the walk is cut at the first lane a search would reach with a higher probe
+// index, and sn_generic_search() continues from there probe by probe, 64 probes per step.
+// Windows outside the conditions under which the shortcut is exact (a candidate that a lane
+// of the same window inserted, a length that is not final, the end of the fragment) are
+// replayed one copy at a time by the scalar walk.  tests/sim/snappy_window_sim.cpp is the
+// same walk with the lanes as arrays.
+constexpr int kSnStride1 = 31;     // highest probe index of a search the windows handle
+constexpr int kSnRegLen = 28;      // match bytes a lane measures from its two register windows
+constexpr int kSnMaxLen = 92;      // ... and with up to 64 more bytes from the source ring
+constexpr uint32_t kSnShortLit = 16;  // literal runs copied by their own lane
+
+enum SnMode { SN_SEARCH = 0, SN_POSTMATCH = 1, SN_FORCED = 2 };
+enum SnStatus { SN_CONTINUE = 0, SN_LAST = 1 };
+
+struct SnFrag : SrcRing {  // + the fragment's source and its LDS ring (win_ring.h)
+  uintptr_t dst;
+  rsrc_t w;       // the fragment's output slot (byte stores; parked lanes write nothing)
+  int n, ip_limit;
+  uint32_t shift;  // 32 - log2(table size)
+  int ip;          // next probe (SN_SEARCH) / end of the last copy (SN_POSTMATCH)
+  int cnt;         // probes already made in the current search
+  int anchor, op;  // next_emit, bytes written
+  int mode;        // how the next window starts
+};
+
+// The search loop of :1015-1031 from probe index `cbase` at position `fwd`, 64 probes per
+// step.  true: a probe verified, P / cand are set and the table holds every probe up to P;
+// false: next_ip passed ip_limit (the remainder follows).
+__device__ __forceinline__ bool sn_generic_search(const SnFrag &b, uint32_t fwd, uint32_t cbase,
+                                                  sn_lds_u16 *table, int lane, int &P_out,
+                                                  int &cand_out) {
+  for (;;) {
+    const uint32_t c = cbase + uint32_t(lane);
+    const uint32_t s = (32u + c) >> 5;
+    const uint32_t incl = sn_incl_scan(s, lane);
+    const uint32_t P = fwd + incl - s, Pn = fwd + incl;
+    const bool valid = int(Pn) <= b.ip_limit;
+    const uint64_t vmask = ballot(valid);
+    const uint32_t seq = valid ? ld32u(b.src + P) : 0u;
+    const uint32_t h = (seq * kSnMul) >> b.shift;
+    uint64_t eq = vmask;
+#pragma unroll
+    for (uint32_t bit = 0; bit < 14u; ++bit) {
+      const bool hb = (h >> bit) & 1u;
+      const uint64_t bm = ballot(hb);
+      eq &= hb ? bm : ~bm;
+    }
+    const uint64_t lower = eq & ((1ull << lane) - 1ull);
+    const int pred = lower ? 63 - __builtin_clzll(lower) : 0;
+    const uint32_t predP = uint32_t(__shfl(int(P), pred));
+    const uint32_t cd = lower ? predP : uint32_t(table[h]);
+    const bool m = valid && ld32u(b.src + cd) == seq;
+    const uint64_t mm = ballot(m);
+    const int f = ffs64(mm);
+    const int e = ffs64(~vmask);
+    if (f < e) {
+      const uint64_t upto = (2ull << f) - 1ull;
+      const uint64_t later = eq & ~((2ull << lane) - 1ull) & upto;
+      if (lane <= f && !later) table[h] = uint16_t(P);
+      P_out = __builtin_amdgcn_readlane(int(P), f);
+      cand_out = __builtin_amdgcn_readlane(int(cd), f);
+      return true;
+    }
+    if (e < 64) return false;
+    {
+      const uint64_t later = eq & ~((2ull << lane) - 1ull);
+      if (!later) table[h] = uint16_t(P);
+    }
+    fwd = uint32_t(__builtin_amdgcn_readlane(int(Pn), 63));
+    cbase += 64u;
+  }
+}
+
+// bytes emit_copy (:718) writes for a copy of `len` bytes at `off`
+__device__ __forceinline__ uint32_t sn_copy_size(uint32_t len, uint32_t off) {
+  const uint32_t k64 = len >= 68u ? (len - 4u) >> 6 : 0u;
+  uint32_t rem = len - (k64 << 6), o = 3u * k64;
+  if (rem > 64u) { o += 3u; rem -= 60u; }
+  return o + ((rem < 12u && off < 2048u) ? 2u : 3u);
+}
+
+__device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand, sn_lds_u16 *table,
+                                              int lane) {
+  const int mode = b.mode;
+  // ---------------------------------------------------------------- per lane
+  const int i = w0 + lane;
+  const bool act = i < b.ip_limit;  // a probe here has next_ip <= ip_limit; a re-test has ip < ip_limit
+  while (b.H < w0 + int(b.sa) + 64 + kSnMaxLen + 8) ring_fill(b, lane);
+  uint32_t xd[9], yt[9];
+  ring_load9(b, (uint32_t(i) + b.sa) & ~3u, xd);
+  const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
+  const uint32_t seq = __builtin_amdgcn_alignbyte(xd[2], xd[1], shi);
+  const uint32_t h = (seq * kSnMul) >> b.shift;
+  int tc = act ? int(table[h]) : 0;
+  if (mode == SN_FORCED && lane == 0) tc = forced_cand;
+  // the candidate's 36 bytes: from the ring when it is that recent, else from memory
+  const uint32_t ac = (uint32_t(tc) + b.sa) & ~3u;
+  const bool far = act && int(ac) - 4 < b.H - int(kRingBytes);
+  ring_load9(b, ac, yt);
+  if (ballot(far)) {
+    uint32_t g[9];
+    load9(b.r, far ? ac : kNoLoad, g);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) yt[k] = far ? g[k] : yt[k];
+  }
+  // lanes with the same hash (the candidate may be a position inserted in this window)
+  const uint64_t ACT = ballot(act);
+  uint64_t eq = ACT;
+#pragma unroll
+  for (uint32_t bit = 0; bit < 14u; ++bit) {
+    const bool hb = (h >> bit) & 1u;
+    const uint64_t bm = ballot(hb);
+    eq &= hb ? bm : ~bm;
+  }
+  if (!act) eq = 0;
+  const uint64_t DUP = ballot((eq & ((1ull << lane) - 1ull)) != 0);
+  const uint32_t shc = (uint32_t(tc) + b.sa) & 3u;
+  const bool tver = act && seq == __builtin_amdgcn_alignbyte(yt[2], yt[1], shc);
+  const uint64_t VT = ballot(tver);
+  int len = kSnRegLen;
+#pragma unroll
+  for (int k = 6; k >= 1; --k) {
+    const uint32_t z = __builtin_amdgcn_alignbyte(xd[k + 2], xd[k + 1], shi) ^
+                       __builtin_amdgcn_alignbyte(yt[k + 2], yt[k + 1], shc);
+    if (z) len = 4 * k + (__builtin_ctz(z) >> 3);
+  }
+  // a match that fills the register window is measured on from the ring, 4 bytes a step, up
+  // to kSnMaxLen; `sat` = the length is still not final and has to be finished from memory if
+  // the parse takes this match
+  bool more = tver && len == kSnRegLen && !far;
+  if (ballot(more)) {
+    const uint32_t vi = uint32_t(i) + b.sa, vc = uint32_t(tc) + b.sa;
+#pragma unroll 1
+    for (int j = 0; j < (kSnMaxLen - kSnRegLen) / 4; ++j) {
+      if (!ballot(more)) break;
+      const uint32_t pi = vi + uint32_t(len), pc = vc + uint32_t(len);
+      ring_lds_u8 *rb = (ring_lds_u8 *)b.ring;
+      const uint32_t a0 = *(ring_lds_u32 *)(rb + (pi & (kRingBytes - 4u)));
+      const uint32_t a1 = *(ring_lds_u32 *)(rb + ((pi + 4u) & (kRingBytes - 4u)));
+      const uint32_t c0 = *(ring_lds_u32 *)(rb + (pc & (kRingBytes - 4u)));
+      const uint32_t c1 = *(ring_lds_u32 *)(rb + ((pc + 4u) & (kRingBytes - 4u)));
+      const uint32_t z = __builtin_amdgcn_alignbyte(a1, a0, pi & 3u) ^
+                         __builtin_amdgcn_alignbyte(c1, c0, pc & 3u);
+      if (more) {
+        len += z ? int(__builtin_ctz(z) >> 3) : 4;
+        if (z) more = false;
+      }
+    }
+  }
+  if (len > b.n - i) len = b.n - i;  // find_match_length stops at the end of the input (:823)
+  const bool sat = tver && i + len < b.n && (len == kSnMaxLen || (far && len == kSnRegLen));
+  const uint32_t back = __builtin_amdgcn_alignbyte(xd[1], xd[0], shi);  // bytes i-4 .. i-1
+  const int NA = ~ACT ? __builtin_ctzll(~ACT) : 64;  // first lane that may not be probed
+
+  // one readlane per copy fetches the lane's candidate, match length and `sat`
+  const uint32_t pk = uint32_t(tc) | (uint32_t(len) << 16) | (sat ? 1u << 27 : 0u);
+  const uint64_t VD = VT | DUP;  // lanes >= NA have neither bit
+
+  const int anchor_in = b.anchor;
+  uint64_t INS = 0, chosen = 0;
+  int L_cand = 0, L_len = 0;  // per lane: the copy that starts here
+  int anchor = b.anchor, cnt = b.cnt;
+  int q = 0, x = 0, cand = 0, ipn = 0;
+  bool inwin = false, ver = false;
+  int st = SN_CONTINUE;
+  b.mode = SN_SEARCH;
+
+  // ------------------------------------------------------------ parallel walk
+  bool fast_done = false;
+  if (NA == 64) {
+    const int e = mode == SN_POSTMATCH ? 1 : 0;
+    const int tl = lane + len;
+    const uint64_t fm = tl >= 64 ? 0ull : VT & (~0ull << tl);
+    const int J0 = fm ? __builtin_ctzll(fm) : 64;
+    // (every lane takes part in each shuffle: a lane that is switched off reads as 0)
+    const int s1 = __shfl(J0, J0 & 63);
+    const int J1 = J0 < 64 ? s1 : 64;
+    const int s2 = __shfl(J1, J1 & 63);
+    const int J2 = J1 < 64 ? s2 : 64;
+    const int s3 = __shfl(J2, J2 & 63);
+    const int J3 = J2 < 64 ? s3 : 64;
+    const uint64_t em = VT & ~bits_below(e);
+    int pos = em ? __builtin_ctzll(em) : 64;  // lane k < 16 looks up the k-th copy
+    {
+      const int p0 = __shfl(J0, pos & 63);
+      if ((lane & 1) && pos < 64) pos = p0;
+      const int p1 = __shfl(J1, pos & 63);
+      if ((lane & 2) && pos < 64) pos = p1;
+      const int p2 = __shfl(J2, pos & 63);
+      if ((lane & 4) && pos < 64) pos = p2;
+      const int p3 = __shfl(J3, pos & 63);
+      if ((lane & 8) && pos < 64) pos = p3;
+    }
+    // OR of (1 << pos) over lanes 0..15: a DPP scan inside the first row
+    uint32_t blo = (lane < 16 && pos < 32) ? 1u << pos : 0u;
+    uint32_t bhi = (lane < 16 && pos >= 32 && pos < 64) ? 1u << (pos - 32) : 0u;
+#define RDK_ROW_OR(v)                                                                  \
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, true));      \
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, true));      \
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, true));      \
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, true));
+    RDK_ROW_OR(blo)
+    RDK_ROW_OR(bhi)
+#undef RDK_ROW_OR
+    uint64_t ch = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(bhi), 15))) << 32) |
+                  uint32_t(__builtin_amdgcn_readlane(int(blo), 15));
+    // per lane: the end of the previous chosen copy
+    const uint64_t lowc = ch & ((1ull << lane) - 1ull);
+    const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
+    const int pend = __shfl(i + len, pl);
+    const bool interior = lowc && pend > i;
+    const uint64_t Mv = ballot(lane >= e && !interior);
+    uint64_t Tm = ballot(lowc && pend == i);
+    uint64_t Rm = ballot(lowc && pend == i + 1 && pend - w0 < 64);
+    if (mode == SN_POSTMATCH) {
+      Tm |= 2ull;
+      Rm |= 1ull;
+    }
+    // probe index of every searched lane: its distance from the last re-tested lane
+    const uint64_t lt = Tm & ((1ull << lane) - 1ull);
+    const int idx = lt ? lane - 1 - (63 - __builtin_clzll(lt)) : b.cnt + lane;
+    const bool searched = ((Mv & ~Tm) >> lane) & 1ull;
+    const uint64_t over = ballot(searched && idx > kSnStride1 && !(mode == SN_FORCED && lane == 0));
+    const int Z = over ? __builtin_ctzll(over) : 64;
+    ch &= bits_below(Z);
+    const uint64_t ins = (Mv | Rm) & bits_below(Z);
+    const bool isch = (ch >> lane) & 1ull;
+    const bool bad = lane < Z && ((isch && (sat || i + len >= b.ip_limit)) ||
+                                  (((Mv >> lane) & 1ull) && (eq & ins & ((1ull << lane) - 1ull))));
+    if (!ballot(bad)) {
+      fast_done = true;
+      INS = ins;
+      chosen = ch;
+      L_cand = tc;
+      L_len = len;
+      int end = -1;
+      if (ch) {
+        const int cl = 63 - __builtin_clzll(ch);
+        end = cl + __builtin_amdgcn_readlane(len, cl);  // lane after the last copy
+        anchor = w0 + end;
+      }
+      if (Z < 64) {
+        b.ip = w0 + Z;
+        b.cnt = kSnStride1 + 1;
+      } else if (end >= 64) {
+        b.ip = w0 + end;
+        b.mode = SN_POSTMATCH;
+      } else {
+        b.ip = w0 + 64;
+        b.cnt = Tm ? 63 - (63 - __builtin_clzll(Tm)) : b.cnt + 64;
+      }
+    }
+  }
+
+  // ------------------------------------------------------------- scalar walk
+  // One loop iteration per copy: the pending match (:1054-1062), then the ip-1 insertion and
+  // the re-test of ip (:1071-1088), then the search for the next match (:1015-1031).
+#define RDK_SN_LOOKUP(lx)                                                                   \
+  do {                                                                                      \
+    const uint64_t eqx = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(eq >> 32), (lx)))) << 32) | \
+                         uint32_t(__builtin_amdgcn_readlane(int(eq), (lx)));                \
+    const uint64_t m_ = eqx & INS & bits_below(lx);                                         \
+    if (m_) {                                                                               \
+      const int j_ = 63 - __builtin_clzll(m_);                                              \
+      cand = w0 + j_;                                                                       \
+      inwin = true;                                                                         \
+      ver = __builtin_amdgcn_readlane(int(seq), j_) == __builtin_amdgcn_readlane(int(seq), (lx)); \
+    } else {                                                                                \
+      inwin = false;                                                                        \
+      ver = (VT >> (lx)) & 1ull;                                                            \
+    }                                                                                       \
+  } while (0)
+  if (!fast_done) {
+    bool have = false;  // a verified match at lane x is pending
+    bool post = false;  // a copy just ended at ipn
+    if (mode == SN_POSTMATCH) {
+      ipn = w0 + 1;
+      post = true;
+    } else if (mode == SN_FORCED) {
+      x = 0;  // lane 0's candidate was set to forced_cand above
+      have = true;
+    }
+    for (;;) {
+      if (have) {
+        have = false;
+        const int P = w0 + x;
+        const uint32_t pkx = uint32_t(__builtin_amdgcn_readlane(int(pk), x));
+        if (!inwin) cand = int(pkx & 0xFFFFu);
+        int fl;
+        if (inwin) {
+          fl = win_count_fwd(b, P + 4, cand + 4, b.n - (P + 4), lane);
+        } else {
+          const int lx = int((pkx >> 16) & 0xFFu);
+          fl = lx - 4;
+          if (pkx & (1u << 27))  // length not final: finish it from the ring / memory
+            fl += win_count_fwd(b, P + lx, cand + lx, b.n - P - lx, lane);
+        }
+        if (lane == x) {
+          L_cand = cand;
+          L_len = 4 + fl;
+        }
+        chosen |= 1ull << x;
+        ipn = P + 4 + fl;
+        anchor = ipn;
+        if (ipn >= b.ip_limit) {  // :1062
+          st = SN_LAST;
+          break;
+        }
+        post = true;
+      }
+      if (post) {
+        post = false;
+        const int r = ipn - 1 - w0;
+        if (r >= 63) {  // the re-test position lies beyond this window
+          b.ip = ipn;
+          b.mode = SN_POSTMATCH;
+          break;
+        }
+        x = r + 1;
+        INS |= 3ull << r;  // table[hash(ip-1)] = ip-1 (:1071) and the re-tested ip itself
+        if ((DUP >> x) & 1ull) {
+          RDK_SN_LOOKUP(x);
+        } else {
+          inwin = false;
+          ver = (VT >> x) & 1ull;
+        }
+        if (ver) {  // immediate copy: no literal
+          have = true;
+          continue;
+        }
+        q = x + 1;
+        cnt = 0;
+      }
+      // search from lane q, whose probe index is cnt; lanes from xlim on have a probe index
+      // above kSnStride1
+      const int xlim = q + (kSnStride1 + 1) - cnt;
+      uint64_t cm = q < 64 ? VD & (~0ull << q) : 0ull;
+      if (xlim < 64) cm &= bits_below(xlim);
+      if (!cm) {  // no candidate left in this window
+        int stop = NA;  // <= 64
+        int why = NA < 64 ? 1 : 0;  // 1: remainder, 0: window end
+        if (xlim <= stop) {         // 2: strides above 1 from here on
+          stop = xlim;
+          why = 2;
+        }
+        INS |= bits_range(q, stop);
+        if (why == 1) {
+          st = SN_LAST;
+        } else {
+          b.ip = w0 + stop;
+          b.cnt = cnt + (stop - q);
+        }
+        break;
+      }
+      x = __builtin_ctzll(cm);
+      INS |= (~0ull << q) & ~(~1ull << x);  // lanes q..x are probed and inserted
+      cnt += x + 1 - q;
+      q = x + 1;
+      if ((DUP >> x) & 1ull) {
+        RDK_SN_LOOKUP(x);
+        have = ver;
+      } else {  // x has no earlier lane with its hash: its table candidate verified (VT)
+        inwin = false;
+        have = true;
+      }
+    }
+  }
+#undef RDK_SN_LOOKUP
+
+  // ------------------------------------------------------------ table update
+  // every inserted lane; the latest position per hash wins
+  if (st != SN_LAST) {
+    const bool ins = (INS >> lane) & 1ull;
+    const uint64_t later = eq & INS & ~bits_below(lane + 1);
+    if (ins && !later) table[h] = uint16_t(i);
+    asm volatile("" ::: "memory");
+  }
+  // ---------------------------------------------------------------- emission
+  // Each chosen lane writes its own literal element (tag, literal bytes) and copy element
+  // at a wave-prefix-sum position.  Every window runs the same store instructions (parked
+  // lanes write nothing).
+  {
+    const bool ch = (chosen >> lane) & 1ull;
+    const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
+    const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
+    const int pend = __shfl(i + L_len, pl);    // end of the previous chosen copy
+    const int prev = lowc ? pend : anchor_in;  // where this copy's literal starts
+    const uint32_t lit = ch ? uint32_t(i - prev) : 0u;
+    const uint32_t off = uint32_t(i - L_cand), ml = uint32_t(L_len);
+    const uint32_t ln = lit - 1u;
+    const uint32_t lhdr = lit == 0u ? 0u : ln < 60u ? 1u : ln < 256u ? 2u : 3u;  // emit_literal (:652)
+    const uint32_t sz = ch ? lhdr + lit + sn_copy_size(ml, off) : 0u;
+    uint32_t tot;
+    const uint32_t tp = uint32_t(b.op) + wave_excl_scan(sz, tot);  // the literal tag
+    const uint32_t lp = tp + lhdr;                                   // first literal byte
+    const uint32_t cp = lp + lit;                                    // the copy element
+    const bool haslit = ch && lit != 0u;
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(ln < 60u ? ln << 2 : (58u + lhdr) << 2), b.w,
+                                         haslit ? tp : kNoLoad, 0, 0);
+    if (ballot(haslit && lhdr > 1u)) {  // literals of more than 60 bytes: length bytes
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(ln), b.w, (haslit && lhdr > 1u) ? tp + 1u : kNoLoad, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(ln >> 8), b.w, (haslit && lhdr > 2u) ? tp + 2u : kNoLoad, 0, 0);
+    }
+    // up to 4 literals sit in the lane's own back dword
+    const bool in_reg = haslit && lit <= 4u;
+    const uint32_t first = 4u - lit;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(back >> (8u * ((first + k) & 3u))), b.w,
+                                           (in_reg && k < lit) ? lp + k : kNoLoad, 0, 0);
+    // the copy element (emit_copy_less_than64, :697); copies of more than 64 bytes below
+    const bool one = ch && ml <= 64u;
+    const bool c2 = ml < 12u && off < 2048u;
+    __builtin_amdgcn_raw_buffer_store_b8(
+        uint8_t(c2 ? 1u + ((ml - 4u) << 2) + ((off >> 8) << 5) : 2u + ((ml - 1u) << 2)), b.w,
+        one ? cp : kNoLoad, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), b.w, one ? cp + 1u : kNoLoad, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), b.w, (one && !c2) ? cp + 2u : kNoLoad, 0, 0);
+    uint64_t bigm = ballot(ch && ml > 64u);  // rare: the whole wave writes the elements (:718)
+    while (bigm) {
+      const int j = __builtin_ctzll(bigm);
+      bigm &= bigm - 1;
+      sn_emit_copy(b.dst + __builtin_amdgcn_readlane(cp, j), __builtin_amdgcn_readlane(off, j),
+                   __builtin_amdgcn_readlane(ml, j), lane);
+    }
+    const uint32_t lstart = uint32_t(prev);
+    const uint32_t la = (lstart + b.sa) & ~3u;
+    const bool need_win = haslit && !in_reg && lit <= kSnShortLit && int(la) >= b.H - int(kRingBytes);
+    if (ballot(need_win)) {  // 5..16 literals: one 20-byte window per lane, from the ring
+      uint32_t wv[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        wv[k] = *(ring_lds_u32 *)((ring_lds_u8 *)b.ring + ((la + 4u * uint32_t(k)) & (kRingBytes - 1u)));
+      const uint32_t sh = (lstart + b.sa) & 3u;
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], sh);
+#pragma unroll
+      for (uint32_t k = 0; k < kSnShortLit; ++k)
+        __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), b.w,
+                                             (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
+    }
+    uint64_t longm = ballot(haslit && !in_reg && !need_win);  // long runs: the whole wave copies them
+    while (longm) {
+      const int j = __builtin_ctzll(longm);
+      longm &= longm - 1;
+      const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
+      const uint32_t jp = __builtin_amdgcn_readlane(lp, j);
+      const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
+      wave_copy_bytes(b.dst + jp, b.src + js, jl, lane);
+    }
+    b.op += int(tot);
+  }
+  b.anchor = anchor;
+  return st;
+}
+
+// compress_fragment (snappy.c:957-1103) in windows; table[0, tsize) is zero.  `cap` = bytes
+// of the output slot.  Returns the size.
+__device__ uint32_t sn_window_fragment(uintptr_t src, uint32_t n, uintptr_t dst, uint32_t cap,
+                                       sn_lds_u16 *table, ring_lds_u32 *ring, uint32_t tsize, int lane) {
+  SnFrag b;
+  ring_init(b, src, n, ring, lane);
+  b.dst = dst;
+  b.w = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(dst), 0, int(cap), 0x00020000);
+  b.n = int(n);
+  b.ip_limit = int(n) - 15;  // kinput_margin_bytes (:965)
+  b.shift = 32u - uint32_t(31 - __builtin_clz(tsize));
+  b.ip = 1;
+  b.cnt = 0;
+  b.anchor = 0;
+  b.op = 0;
+  b.mode = SN_SEARCH;
+  if (n >= 15u) {
+    int forced = 0;
+    for (;;) {
+      int w0;
+      if (b.mode == SN_SEARCH && b.cnt > kSnStride1) {  // strides above 1: probe by probe
+        int P, cand;
+        if (!sn_generic_search(b, uint32_t(b.ip), uint32_t(b.cnt), table, lane, P, cand)) break;
+        asm volatile("" ::: "memory");
+        b.mode = SN_FORCED;
+        forced = cand;
+        w0 = P;
+      } else {
+        w0 = b.mode == SN_POSTMATCH ? b.ip - 1 : b.ip;
+      }
+      if (sn_window_step(b, w0, forced, table, lane) == SN_LAST) break;
+    }
+  }
+  uint32_t op = uint32_t(b.op);
+  if (uint32_t(b.anchor) < n)  // emit_remainder (:1097)
+    op += sn_emit_literal(dst + op, src + uint32_t(b.anchor), n - uint32_t(b.anchor), lane);
+  return op;
+}
+
 // One wavefront per fragment; items are slot-major so that every shader engine is busy.
+template <bool WINDOWS>
 __global__ __launch_bounds__(64) void snappy_compress_fragments_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ out_offs, uint32_t n) {
-  __shared__ uint16_t table_mem[kSnMaxTable];
-  sn_lds_u16 *table = (sn_lds_u16 *)table_mem;
+  // the source ring (windowed engine) sits in front of the hash table
+  constexpr uint32_t kRingLds = WINDOWS ? kRingBytes : 0u;
+  __shared__ __attribute__((aligned(16))) uint8_t lds_mem[kRingLds + 2u * kSnMaxTable];
+  sn_lds_u16 *table = (sn_lds_u16 *)reinterpret_cast<uint16_t *>(lds_mem + kRingLds);
   const int lane = threadIdx.x;
   const uint32_t items = n * uint32_t(kSnItems);
   for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
@@ -247,12 +760,15 @@ __global__ __launch_bounds__(64) void snappy_compress_fragments_kernel(
       const uint32_t fn = len - k * kSnBlock < kSnBlock ? len - k * kSnBlock : kSnBlock;
       uint32_t tsize = 256;  // get_hash_table, snappy.c:790-807
       while (tsize < kSnMaxTable && tsize < fn) tsize <<= 1;
-      for (uint32_t i = uint32_t(lane); i < tsize; i += 64u) table[i] = 0;
+      for (uint32_t i = uint32_t(lane); i < tsize / 2u; i += 64u) ((ring_lds_u32 *)table)[i] = 0;
       asm volatile("" ::: "memory");
       const uintptr_t src = reinterpret_cast<uintptr_t>(in) + in_offs[f] + uint64_t(k) * kSnBlock;
       const uintptr_t slot =
           reinterpret_cast<uintptr_t>(out) + out_offs[f] + kSnSlot0 + uint64_t(k) * kSnSlot;
-      const uint32_t sz = sn_compress_fragment(src, fn, slot + 4u, table, tsize, lane);
+      // (the output resource ends inside rd_kafka_snappy_max_compressed_length of the stream)
+      const uint32_t sz = WINDOWS ? sn_window_fragment(src, fn, slot + 4u, fn + fn / 6u + 16u, table,
+                                                       (ring_lds_u32 *)lds_mem, tsize, lane)
+                                  : sn_compress_fragment(src, fn, slot + 4u, table, tsize, lane);
       if (lane == 0) {
         stb(slot, sz & 0xFFu); stb(slot + 1, (sz >> 8) & 0xFFu);
         stb(slot + 2, (sz >> 16) & 0xFFu); stb(slot + 3, sz >> 24);
@@ -587,8 +1103,14 @@ int snappy_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const
   if (n > 0xFFFFFFFFu / kSnItems) return set_error(RDK_HIP_E_INVAL, "too many streams");
   const uint64_t items = uint64_t(n) * kSnItems;
   const unsigned grid = unsigned(items < 65536u ? items : 65536u);
-  hipLaunchKernelGGL(snappy_compress_fragments_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
-                     d_in_lens, d_out, d_out_offs, n);
+  // RDK_HIP_SNAPPY_SEQ=1 selects the one-copy-at-a-time engine (A/B runs)
+  static const bool seq = [] { const char *e = getenv("RDK_HIP_SNAPPY_SEQ"); return e && *e == '1'; }();
+  if (seq)
+    hipLaunchKernelGGL(snappy_compress_fragments_kernel<false>, dim3(grid), dim3(64), 0, s, d_in,
+                       d_in_offs, d_in_lens, d_out, d_out_offs, n);
+  else
+    hipLaunchKernelGGL(snappy_compress_fragments_kernel<true>, dim3(grid), dim3(64), 0, s, d_in,
+                       d_in_offs, d_in_lens, d_out, d_out_offs, n);
   hipLaunchKernelGGL(snappy_assemble_kernel, dim3(n < 4096u ? n : 4096u), dim3(256), 0, s, d_in_lens,
                      d_out, d_out_offs, d_out_lens, n);
   RDK_HIP_CHECK(hipGetLastError());

@@ -81,6 +81,20 @@ def test_batch_compress_matches_oracle_and_an_independent_decoder(engine, oracle
             assert pa.decompress(c, decompressed_size=len(d), codec="snappy", asbytes=True) == d, i
 
 
+def test_batch_compress_window_shapes(engine, oracle_mod):
+    """the input families of the host model's test (tests/test_snappy_window_sim.py): in-window
+    repeats, literal runs around the stride-1 limit, sparse matches, runs, every edge size --
+    as single fragments and glued into multi-fragment streams"""
+    from test_snappy_window_sim import _inputs
+    frags = _inputs(7, 260)
+    rnd = random.Random(8)
+    glued = [b"".join(rnd.choice(frags) for _ in range(rnd.randrange(2, 6))) for _ in range(40)]
+    inputs = frags + glued
+    got = _compress_batch(engine, inputs)
+    for i, (d, c) in enumerate(zip(inputs, got)):
+        assert c == oracle_mod.snappy_compress(d), (i, len(d), len(c))
+
+
 def test_dropin_compress_iov_segments(engine, oracle_mod):
     rnd = random.Random(3)
     data = W.gen_json(300001, 3)

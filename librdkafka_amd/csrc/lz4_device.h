@@ -38,6 +38,21 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_bal
 
 __device__ __forceinline__ int ffs64(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
 
+// Lanes of `among` whose NBITS-bit value h equals this lane's: one ballot per bit, and per
+// bit and mask half one v_bitop3_b32 (eq & ~(ballot ^ own bit), truth table 0x90).
+template <int NBITS>
+__device__ __forceinline__ uint64_t same_value_lanes(uint32_t h, uint64_t among) {
+  uint32_t lo = uint32_t(among), hi = uint32_t(among >> 32);
+#pragma unroll
+  for (int bit = 0; bit < NBITS; ++bit) {
+    const int m = __builtin_amdgcn_sbfe(int(h), bit, 1);  // 0 or -1
+    const uint64_t bm = ballot(m < 0);
+    lo = __builtin_amdgcn_bitop3_b32(lo, uint32_t(bm), uint32_t(m), 0x90);
+    hi = __builtin_amdgcn_bitop3_b32(hi, uint32_t(bm >> 32), uint32_t(m), 0x90);
+  }
+  return (uint64_t(hi) << 32) | lo;
+}
+
 // XXH32 (xxhash.c) over [p, p+len) by one lane; used only for frames that
 // carry block/content checksums (never set by librdkafka's own frames).
 __device__ inline uint32_t xxh32_lane(uintptr_t p, uint64_t len, uint32_t seed) {

@@ -152,13 +152,7 @@ __device__ int compress_block(uintptr_t src, int n, uintptr_t dst, int accel, ld
         const uint64_t vmask = ballot(valid);
         const uint32_t seq = valid ? ld32u(src + uint32_t(P)) : 0u;
         const uint32_t h = lz4_hash(seq);
-        uint64_t eq = vmask;
-#pragma unroll
-        for (uint32_t bit = 0; bit < kHashLog; ++bit) {
-          const bool hb = (h >> bit) & 1u;
-          const uint64_t bm = ballot(hb);
-          eq &= hb ? bm : ~bm;
-        }
+        uint64_t eq = same_value_lanes<int(kHashLog)>(h, vmask);
         const uint64_t lower = eq & ((1ull << lane) - 1ull);
         const int pred = lower ? 63 - __builtin_clzll(lower) : 0;
         const int predP = __shfl(P, pred);
@@ -287,13 +281,7 @@ __device__ __forceinline__ bool generic_search(uintptr_t src, int mflimitPlusOne
     const uint64_t vmask = ballot(valid);
     const uint32_t seq = valid ? ld32u(src + uint32_t(P)) : 0u;
     const uint32_t h = lz4_hash(seq);
-    uint64_t eq = vmask;
-#pragma unroll
-    for (uint32_t bit = 0; bit < kHashLog; ++bit) {
-      const bool hb = (h >> bit) & 1u;
-      const uint64_t bm = ballot(hb);
-      eq &= hb ? bm : ~bm;
-    }
+    uint64_t eq = same_value_lanes<int(kHashLog)>(h, vmask);
     const uint64_t lower = eq & ((1ull << lane) - 1ull);
     const int pred = lower ? 63 - __builtin_clzll(lower) : 0;
     const int predP = __shfl(P, pred);
@@ -368,13 +356,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   }
   // lanes with the same hash (the candidate may be a position inserted in this window)
   const uint64_t ACT = ballot(act);
-  uint64_t eq = ACT;
-#pragma unroll
-  for (uint32_t bit = 0; bit < kHashLog; ++bit) {
-    const bool hb = (h >> bit) & 1u;
-    const uint64_t bm = ballot(hb);
-    eq &= hb ? bm : ~bm;
-  }
+  uint64_t eq = same_value_lanes<int(kHashLog)>(h, ACT);
   if (!act) eq = 0;
   const uint64_t DUP = ballot((eq & ((1ull << lane) - 1ull)) != 0);
   const uint32_t shc = (uint32_t(tc) + b.sa) & 3u;

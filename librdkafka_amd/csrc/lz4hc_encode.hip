@@ -178,13 +178,7 @@ __device__ void hc_build(const HcBlock &b, int npos) {
     const uint32_t h = valid ? hc_hash(w_next) : 0u;
     w_next = p + 64 < npos ? ld32u(b.s + p + 64) : 0u;
     if (valid) b.tr[p] = h;  // the scatter below reads the hash back from here
-    uint64_t eq = ballot(valid);
-#pragma unroll
-    for (int bit = 0; bit < kHcHashLog; ++bit) {
-      const bool on = (h >> bit) & 1u;
-      const uint64_t m = ballot(on);
-      eq &= on ? m : ~m;
-    }
+    const uint64_t eq = same_value_lanes<kHcHashLog>(h, ballot(valid));
     const uint32_t hv = valid ? b.head[h] : kHcNone;
     const uint64_t eb = eq & below;
     const uint32_t rk = (hv == kHcNone ? 0u : (hv >> 16) + 1u) + uint32_t(__popcll(eb));

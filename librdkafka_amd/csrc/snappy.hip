@@ -172,13 +172,7 @@ __device__ uint32_t sn_compress_fragment(uintptr_t src, uint32_t n, uintptr_t ds
           const uint64_t vmask = ballot(valid);
           const uint32_t seq = valid ? ld32u(src + P) : 0u;
           const uint32_t h = (seq * kSnMul) >> shift;
-          uint64_t eq = vmask;
-#pragma unroll
-          for (uint32_t bit = 0; bit < 14u; ++bit) {
-            const bool hb = (h >> bit) & 1u;
-            const uint64_t bm = ballot(hb);
-            eq &= hb ? bm : ~bm;
-          }
+          uint64_t eq = same_value_lanes<14>(h, vmask);
           const uint64_t lower = eq & ((1ull << lane) - 1ull);
           const int pred = lower ? 63 - __builtin_clzll(lower) : 0;
           const uint32_t predP = uint32_t(__shfl(int(P), pred));
@@ -284,13 +278,7 @@ __device__ __forceinline__ bool sn_generic_search(const SnFrag &b, uint32_t fwd,
     const uint64_t vmask = ballot(valid);
     const uint32_t seq = valid ? ld32u(b.src + P) : 0u;
     const uint32_t h = (seq * kSnMul) >> b.shift;
-    uint64_t eq = vmask;
-#pragma unroll
-    for (uint32_t bit = 0; bit < 14u; ++bit) {
-      const bool hb = (h >> bit) & 1u;
-      const uint64_t bm = ballot(hb);
-      eq &= hb ? bm : ~bm;
-    }
+    uint64_t eq = same_value_lanes<14>(h, vmask);
     const uint64_t lower = eq & ((1ull << lane) - 1ull);
     const int pred = lower ? 63 - __builtin_clzll(lower) : 0;
     const uint32_t predP = uint32_t(__shfl(int(P), pred));
@@ -351,13 +339,7 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
   }
   // lanes with the same hash (the candidate may be a position inserted in this window)
   const uint64_t ACT = ballot(act);
-  uint64_t eq = ACT;
-#pragma unroll
-  for (uint32_t bit = 0; bit < 14u; ++bit) {
-    const bool hb = (h >> bit) & 1u;
-    const uint64_t bm = ballot(hb);
-    eq &= hb ? bm : ~bm;
-  }
+  uint64_t eq = same_value_lanes<14>(h, ACT);
   if (!act) eq = 0;
   const uint64_t DUP = ballot((eq & ((1ull << lane) - 1ull)) != 0);
   const uint32_t shc = (uint32_t(tc) + b.sa) & 3u;

@@ -30,6 +30,16 @@ __device__ __forceinline__ uint32_t ld32u(uintptr_t a) {
   return __builtin_amdgcn_alignbyte(hi, lo, uint32_t(a & 3u));
 }
 
+// the same through two unconditional loads (no branch, so the loads can stay in flight
+// across the code that follows); the caller guarantees that the dword behind the one holding
+// byte a may be read
+__device__ __forceinline__ uint32_t ld32u_nb(uintptr_t a) {
+  const uintptr_t b = a & ~uintptr_t(3);
+  const uint32_t lo = *(g_cu32 *)b;
+  const uint32_t hi = *(g_cu32 *)(b + 4);
+  return __builtin_amdgcn_alignbyte(hi, lo, uint32_t(a & 3u));
+}
+
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // lane mask of a predicate, straight from the compare (HIP's __ballot takes an int and

@@ -48,6 +48,7 @@
 
 #include "common.h"
 #include "lz4_device.h"
+#include "lz4_wave.h"
 
 namespace rdk {
 
@@ -447,12 +448,12 @@ __device__ __forceinline__ bool hc_sure_miss(const HcBlock &b, int p, int mflimi
 
 // LZ4HC_compress_hashChain (lz4hc.c:532-746).  Returns the compressed size or
 // 0 when the block does not fit in n-1 bytes.  n >= 13.
-__device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n) {
+__device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool prebuilt) {
   const int mflimit = n - kLz4MFLimit, matchlimit = n - kLz4LastLiterals, oend = n - 1;
 #ifdef RDK_HC_PROF
   const uint64_t t0 = wall_clock64();
 #endif
-  hc_build(b, mflimit + 1);
+  if (!prebuilt) hc_build(b, mflimit + 1);
 #ifdef RDK_HC_PROF
   const uint64_t t1 = wall_clock64();
   int nskip = 0;
@@ -656,10 +657,11 @@ __device__ __forceinline__ void hc_opt_trailing(const HcBlock &b, int last, int 
 
 // LZ4HC_compress_optimal (lz4hc.c:1278-1538), limitedOutput.  Returns the compressed
 // size or 0 when the block does not fit in n-1 bytes.  n >= 13.
-__device__ int hc_optimal_block(const HcBlock &b, uintptr_t dst, int n, int sufficient, bool full) {
+__device__ int hc_optimal_block(const HcBlock &b, uintptr_t dst, int n, int sufficient, bool full,
+                                bool prebuilt) {
   const int mflimit = n - kLz4MFLimit, matchlimit = n - kLz4LastLiterals, oend = n - 1;
   const int lane = b.lane;
-  hc_build(b, mflimit + 1);
+  if (!prebuilt) hc_build(b, mflimit + 1);
   if (sufficient >= kHcOptNum) sufficient = kHcOptNum - 1;
   int ip = 0, anchor = 0, op = 0;
   while (ip <= mflimit) {
@@ -783,23 +785,173 @@ __device__ int hc_optimal_block(const HcBlock &b, uintptr_t dst, int n, int suff
   return op;
 }
 
+// real_items = n * (blocks of the longest frame): the slot-major items at or past it are the
+// empty block slots of short frames, and a chunk made of them only is skipped.
+__global__ __launch_bounds__(256) void lz4hc_count_items_kernel(const uint32_t *__restrict__ in_lens,
+                                                                uint32_t n, uint32_t *real_items) {
+  __shared__ uint32_t wmax[4];
+  uint32_t m = 0;
+  for (uint32_t f = threadIdx.x; f < n; f += 256u) {
+    const uint32_t nb = (in_lens[f] + kLz4Block - 1) / kLz4Block;
+    m = nb > m ? nb : m;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t o = uint32_t(__shfl_xor(int(m), d));
+    m = o > m ? o : m;
+  }
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) m = wmax[w] > m ? wmax[w] : m;
+    const uint64_t r = uint64_t(m < uint32_t(kHcItems) ? m : uint32_t(kHcItems)) * n;
+    *real_items = uint32_t(r);
+  }
+}
+
+// The build phase for the first block of every item of [it0, it1), with the hash heads on
+// chip: one workgroup per block, head[] (last position and bucket rank per hash, 128 KiB) in
+// LDS.  Wave 0 runs the ordered pass over the positions (hash chain delta and rank inside the
+// hash bucket, 64 positions per step); all waves then turn the bucket sizes into bucket
+// starts and scatter the positions into `sorted`.  Everything that goes to memory is a
+// coalesced stream except the u16 scatter into the block's own 128 KiB `sorted`.  (A wave
+// that builds in its own HBM scratch, hc_build(), reads and rewrites a random 64-byte line
+// of a 128 KiB table per position: with thousands of waves resident that was most of the
+// engine's memory traffic.)
+constexpr int kHcBuildThreads = 1024;
+constexpr int kHcAhead = 8;  // source words in flight per lane of the ordered pass
+
+__global__ __launch_bounds__(kHcBuildThreads) void lz4hc_build_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
+    const uint32_t *__restrict__ in_lens, uint32_t n, uint8_t *scratch, uint32_t it0, uint32_t it1,
+    const uint32_t *__restrict__ real_items) {
+  if (it0 >= *real_items) return;  // every item of this chunk is an empty block slot
+  __shared__ uint32_t head[1 << kHcHashLog];
+  __shared__ uint32_t part[kHcBuildThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int kWaves = kHcBuildThreads / 64;
+  for (uint32_t it = it0 + blockIdx.x; it < it1; it += gridDim.x) {
+    const uint32_t f = it % n, k = it / n;
+    const uint32_t len = in_lens[f];
+    const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
+    if (k >= nb) continue;
+    const uint32_t bn = (len - k * kLz4Block) < kLz4Block ? (len - k * kLz4Block) : kLz4Block;
+    if (bn < uint32_t(kLz4MFLimit + 1)) continue;
+    const int npos = int(bn) - kLz4MFLimit + 1;  // positions 0 .. mflimit
+    const uintptr_t s = reinterpret_cast<uintptr_t>(in) + in_offs[f] + uint64_t(k) * kLz4Block;
+    uint8_t *sc = scratch + size_t(it - it0) * kHcScratch;
+    uint16_t *chain = reinterpret_cast<uint16_t *>(sc + kHcTab);
+    uint16_t *sorted = chain + 2 * 65536;
+    uint32_t *tr = reinterpret_cast<uint32_t *>(sorted + 65536);
+    for (int i = tid; i < (1 << kHcHashLog); i += kHcBuildThreads) head[i] = kHcNone;
+    __syncthreads();
+    if (wave == 0) {
+      const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+      const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+      // the source words of the next kHcAhead steps are in flight (they do not depend on
+      // the head[] updates), so a step waits on LDS only; a position below npos has at
+      // least 11 block bytes behind it, so the branch-free 8-byte read stays inside
+      // (kept as raw dword pairs and aligned at the use, so that no step waits for a
+      // load issued after its own)
+      uint32_t wl[kHcAhead], wh[kHcAhead];
+      const uint32_t sh = uint32_t((s + lane) & 3u);
+#pragma unroll
+      for (int j = 0; j < kHcAhead; ++j) {
+        const uintptr_t a = (s + min(lane + 64 * j, npos - 1)) & ~uintptr_t(3);
+        wl[j] = *(g_cu32 *)a;
+        wh[j] = *(g_cu32 *)(a + 4);
+      }
+      for (int base0 = 0; base0 < npos; base0 += 64 * kHcAhead) {
+#pragma unroll
+        for (int j = 0; j < kHcAhead; ++j) {
+          const int base = base0 + 64 * j;
+          const int p = base + lane;
+          const bool valid = p < npos;
+          const uint32_t h = valid ? hc_hash(__builtin_amdgcn_alignbyte(wh[j], wl[j], sh)) : 0u;
+          {  // (clamped, not predicated: a predicated load is waited for at once)
+            const uintptr_t a = (s + min(p + 64 * kHcAhead, npos - 1)) & ~uintptr_t(3);
+            wl[j] = *(g_cu32 *)a;
+            wh[j] = *(g_cu32 *)(a + 4);
+          }
+          const uint64_t eq = same_value_lanes<kHcHashLog>(h, ballot(valid));
+          const uint32_t hv = valid ? head[h] : kHcNone;
+          const uint64_t eb = eq & below;
+          const uint32_t rk = (hv == kHcNone ? 0u : (hv >> 16) + 1u) + uint32_t(__popcll(eb));
+          int prev;
+          if (eb) prev = base + (63 - __clzll(eb));
+          else prev = hv == kHcNone ? -65536 : int(hv & 0xFFFFu);
+          if (valid) {
+            const int d = p - prev;  // LZ4HC_Insert (lz4hc.c:125-132)
+            chain[p] = uint16_t(d > 65535 ? 65535 : d);
+            tr[p] = h | (rk << 16);  // the scatter below takes hash and rank from here
+            if (!(eq & above)) head[h] = uint32_t(p) | (rk << 16);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // bucket sizes -> bucket starts: every wave sums its quarter of the table, then scans it
+    // row by row from the sum of the quarters before it
+    constexpr int kRows = (1 << kHcHashLog) / 64 / kWaves;
+    uint32_t *mine = head + wave * kRows * 64;
+    uint32_t sum = 0;
+    for (int r = 0; r < kRows; ++r) {
+      const uint32_t v = mine[r * 64 + lane];
+      sum += v == kHcNone ? 0u : (v >> 16) + 1u;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
+    if (lane == 0) part[wave] = sum;
+    __syncthreads();
+    uint32_t run = 0;
+    for (int w = 0; w < wave; ++w) run += part[w];
+    for (int r = 0; r < kRows; ++r) {
+      const uint32_t v = mine[r * 64 + lane];
+      const uint32_t c = v == kHcNone ? 0u : (v >> 16) + 1u;
+      uint32_t tot;
+      const uint32_t excl = wave_excl_scan(c, tot);
+      mine[r * 64 + lane] = run + excl;
+      run += tot;
+    }
+    __syncthreads();
+    // scatter, four steps' loads issued before their stores
+    for (int p0 = tid; p0 < npos; p0 += 4 * kHcBuildThreads) {
+      uint32_t t[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = p0 + kHcBuildThreads * j;
+        t[j] = p < npos ? tr[p] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = p0 + kHcBuildThreads * j;
+        if (p < npos) {
+          const uint32_t r = t[j] >> 16;
+          const uint32_t idx = head[t[j] & 0x7FFFu] + r;
+          sorted[idx] = uint16_t(p);
+          tr[p] = idx | (r << 16);
+        }
+      }
+    }
+    __syncthreads();  // head[] is reused by the next item
+  }
+}
+
 // OPT: the optimal parser (levels 10..12), a kernel of its own so that its registers do
-// not cost the hash-chain parser its residency.
+// not cost the hash-chain parser its residency.  Items [it0, it1) come from a work queue;
+// item `it` has its tables at scratch + (it - it0) * kHcScratch, built by lz4hc_build_kernel
+// for its first block (frames of more than 64 blocks: the wave builds the further ones
+// itself, in the same tables).
 template <bool OPT>
 __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ out_offs, uint32_t n, int attempts, int sufficient,
-    uint8_t *scratch, uint32_t *__restrict__ next_item) {
+    uint8_t *scratch, uint32_t *__restrict__ next_item, uint32_t it0, uint32_t it1,
+    const uint32_t *__restrict__ real_items) {
+  if (it0 >= *real_items) return;  // every item of this chunk is an empty block slot
   HcBlock b;
   b.lane = threadIdx.x;
-  uint8_t *sc = scratch + size_t(blockIdx.x) * kHcScratch;
-  b.head = reinterpret_cast<uint32_t *>(sc);
-  b.chain = reinterpret_cast<uint16_t *>(sc + kHcTab);
-  b.rank = b.chain + 65536;
-  b.sorted = b.rank + 65536;
-  b.tr = reinterpret_cast<uint32_t *>(b.sorted + 65536);
-  b.opt = reinterpret_cast<int4 *>(b.tr + 65536);
   b.attempts = attempts;
   // the optimal parser always searches with pattern analysis (lz4hc.c:1267), the
   // hash-chain parser from level 9 (lz4hc.c:544)
@@ -808,12 +960,18 @@ __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
   // the next item when it finishes one, so the parse's uneven cost per block
   // spreads over the whole grid; the empty slots of short frames come last
   // and cost one atomic each.
-  const uint32_t items = n * uint32_t(kHcItems);
   for (;;) {
     uint32_t it = 0;
     if (b.lane == 0) it = atomicAdd(next_item, 1u);
-    it = uni(it);
-    if (it >= items) break;
+    it = it0 + uni(it);
+    if (it >= it1) break;
+    uint8_t *sc = scratch + size_t(it - it0) * kHcScratch;
+    b.head = reinterpret_cast<uint32_t *>(sc);
+    b.chain = reinterpret_cast<uint16_t *>(sc + kHcTab);
+    b.rank = b.chain + 65536;
+    b.sorted = b.rank + 65536;
+    b.tr = reinterpret_cast<uint32_t *>(b.sorted + 65536);
+    b.opt = reinterpret_cast<int4 *>(b.tr + 65536);
     const uint32_t f = it % n, kk = it / n;
     const uint32_t len = uni(in_lens[f]);
     const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
@@ -826,8 +984,8 @@ __global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
       // and its last-literals run cannot fit either)
       int csize = 0;
       if (bn >= uint32_t(kLz4MFLimit + 1))
-        csize = OPT ? hc_optimal_block(b, slot + 4u, int(bn), sufficient, attempts == 16384)
-                    : hc_compress_block(b, slot + 4u, int(bn));
+        csize = OPT ? hc_optimal_block(b, slot + 4u, int(bn), sufficient, attempts == 16384, k == kk)
+                    : hc_compress_block(b, slot + 4u, int(bn), k == kk);
       if (b.lane == 0) {
         const uint32_t w = csize ? uint32_t(csize) : (bn | 0x80000000u);  // LZ4F_makeBlock
         stb(slot, w & 0xFFu); stb(slot + 1, (w >> 8) & 0xFFu);
@@ -842,9 +1000,10 @@ void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const 
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, hipStream_t s, const FuseCrc *fuse);
 
-// The hash/chain tables (kHcScratch bytes per wave) and the work-queue counter live in
-// the calling thread's kScratchHc region: calls on different streams are ordered by
-// scratch_acquire / scratch_release, so two streams never share the tables.
+// The hash/chain tables (kHcScratch bytes per item of a chunk) and the work-queue counters
+// live in the calling thread's kScratchHc region: calls on different streams are ordered by
+// scratch_acquire / scratch_release, so two streams never share the tables.  A batch runs
+// in chunks of kHcGrid items: the build kernel, then the parser on one wave per item.
 int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, int level, hipStream_t s) {
@@ -852,24 +1011,35 @@ int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const 
   if (n > (0xFFFFFFFFu / kHcItems) - kHcGrid) return set_error(RDK_HIP_E_INVAL, "too many frames");
   Ctx *c = ctx();
   if (!c) return RDK_HIP_E_NODEV;
-  const uint64_t items = uint64_t(n) * kHcItems;
-  const unsigned grid = unsigned(items < kHcGrid ? items : kHcGrid);
-  // a single drop-in frame needs 64 slices, a large batch the full grid
-  int rc = scratch_acquire(c, kScratchHc, size_t(kHcScratch) * grid + 256, s);
+  const uint32_t items = n * uint32_t(kHcItems);
+  const uint32_t chunk = items < kHcGrid ? items : kHcGrid;  // a single drop-in frame: 64 items
+  const uint32_t nchunks = (items + chunk - 1) / chunk;
+  const size_t counters = (size_t(nchunks + 1) * sizeof(uint32_t) + 255) & ~size_t(255);
+  int rc = scratch_acquire(c, kScratchHc, size_t(kHcScratch) * chunk + counters, s);
   if (rc) return rc;
   uint8_t *p = c->d_stage[kScratchHc];
   // clTable (lz4hc.c:775-789): nbSearches, and the optimal parser's sufficient length
   if (level > 12) level = 12;  // MIN(LZ4HC_CLEVEL_MAX, cLevel), lz4hc.c:798
   const int attempts = level >= 12 ? 16384 : level == 11 ? 512 : level == 10 ? 96 : 1 << (level - 1);
   const int sufficient = level >= 12 ? kHcOptNum : level == 11 ? 128 : level == 10 ? 64 : 0;
-  uint32_t *next_item = reinterpret_cast<uint32_t *>(p + size_t(kHcScratch) * grid);
-  RDK_HIP_CHECK(hipMemsetAsync(next_item, 0, sizeof(uint32_t), s));
-  if (sufficient)
-    hipLaunchKernelGGL(lz4hc_compress_blocks_kernel<true>, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
-                       d_in_lens, d_out, d_out_offs, n, attempts, sufficient, p, next_item);
-  else
-    hipLaunchKernelGGL(lz4hc_compress_blocks_kernel<false>, dim3(grid), dim3(64), 0, s, d_in,
-                       d_in_offs, d_in_lens, d_out, d_out_offs, n, attempts, sufficient, p, next_item);
+  uint32_t *next_item = reinterpret_cast<uint32_t *>(p + size_t(kHcScratch) * chunk);
+  RDK_HIP_CHECK(hipMemsetAsync(next_item, 0, size_t(nchunks) * sizeof(uint32_t), s));
+  uint32_t *real_items = next_item + nchunks;
+  hipLaunchKernelGGL(lz4hc_count_items_kernel, dim3(1), dim3(256), 0, s, d_in_lens, n, real_items);
+  for (uint32_t ci = 0; ci < nchunks; ++ci) {
+    const uint32_t it0 = ci * chunk, it1 = it0 + chunk < items ? it0 + chunk : items;
+    const unsigned grid = it1 - it0;
+    hipLaunchKernelGGL(lz4hc_build_kernel, dim3(grid), dim3(kHcBuildThreads), 0, s, d_in, d_in_offs,
+                       d_in_lens, n, p, it0, it1, real_items);
+    if (sufficient)
+      hipLaunchKernelGGL(lz4hc_compress_blocks_kernel<true>, dim3(grid), dim3(64), 0, s, d_in,
+                         d_in_offs, d_in_lens, d_out, d_out_offs, n, attempts, sufficient, p,
+                         next_item + ci, it0, it1, real_items);
+    else
+      hipLaunchKernelGGL(lz4hc_compress_blocks_kernel<false>, dim3(grid), dim3(64), 0, s, d_in,
+                         d_in_offs, d_in_lens, d_out, d_out_offs, n, attempts, sufficient, p,
+                         next_item + ci, it0, it1, real_items);
+  }
   lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s, nullptr);
   RDK_HIP_CHECK(hipGetLastError());
   return scratch_release(c, kScratchHc, s);

@@ -116,3 +116,12 @@ def test_batch_hc_many_frames_queue_and_scratch_growth(engine, oracle_mod):
         fl = out_lens.cpu().numpy()
         for i in range(len(inputs)):
             assert host[i * bound:i * bound + fl[i]] == want[i % 4], (len(inputs), i)
+
+
+@pytest.mark.parametrize("level", [4, 10])
+def test_hc_frame_of_more_than_64_blocks(engine, oracle_mod, level):
+    """a 4.3 MiB frame has 66 blocks: the parser's wave builds the tables of blocks 64 and 65
+    itself (the build kernel serves the first block of each of the 64 block slots)"""
+    data = W.gen_json(64 * 65536 + 70000, 17)
+    err, fr = engine.rd_kafka_lz4_compress(1, level, data)
+    assert err == 0 and fr == oracle_mod.rdk_lz4_compress(data, comp_level=level)[1]

@@ -334,38 +334,62 @@ __device__ int hc_search_serial(const HcBlock &b, int ip, int ilow, int ihigh, i
   return longest;
 }
 
+// LZ4HC_countBack (lz4hc.c:140-152) by one lane: equal bytes walking back from ip-1 / c-1,
+// at most -lim of them (lim <= 0), four per dependent round trip.  Returns -count.
+__device__ __forceinline__ int hc_count_back(uintptr_t s, int ip, int c, int lim) {
+  int back = 0;
+  while (back - 4 >= lim) {
+    const uint32_t x = ld32u_nb(s + ip + back - 4) ^ ld32u_nb(s + c + back - 4);
+    if (x) return back - (__builtin_clz(x) >> 3);
+    back -= 4;
+  }
+  while (back > lim && ldb(s + ip + back - 1) == ldb(s + c + back - 1)) back--;
+  return back;
+}
+
 // LZ4HC_InsertAndGetWiderMatch, 64 chain candidates per step
 __device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int longest, int &mpos,
                          int &spos) {
   const uintptr_t s = b.s;
   const int lane = b.lane;
-  const uint32_t pat = ld32u(s + ip);
+  // (ip <= mflimit: the branch-free 8-byte read stays inside the block, and the table entry
+  // is in flight together with the pattern)
+  const uint32_t pat = ld32u_nb(s + ip);
+  const uint32_t t = b.tr[ip];  // one load instead of rank -> hash -> bucket start
   if (b.pa && ((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24)))
     return hc_search_serial(b, ip, ilow, ihigh, longest, mpos, spos, pat, false);
   const int br = ip - ilow;
-  const uint32_t t = b.tr[ip];  // one load instead of rank -> hash -> bucket start
   const int r = int(t >> 16);
   const int top = int(t & 0xFFFFu) - 1;  // sorted[top] = latest earlier same-hash
   const int total = r < b.attempts ? r : b.attempts;
   for (int c0 = 0; c0 < total; c0 += 64) {
     const int j = c0 + lane;
     const bool valid = j < total;
-    const int c = valid ? int(b.sorted[top - j]) : 0;
-    const bool ok32 = valid && ld32u(s + c) == pat;
+    const int c = int(b.sorted[valid ? top - j : top]);
+    const bool ok32 = (ld32u_nb(s + c) == pat) & valid;  // (c < ip: inside the block as well)
     int back = 0, len = 0;
     if (ok32) {
-      if (br) {  // LZ4HC_countBack (lz4hc.c:140-152)
+      if (br) {
         const int lim = (ilow - ip) > -c ? (ilow - ip) : -c;
-        while (back > lim && ldb(s + ip + back - 1) == ldb(s + c + back - 1)) back--;
+        back = hc_count_back(s, ip, c, lim);
       }
       len = 4 + hc_count(s, ip + 4, c + 4, ihigh) - back;
     }
     int k0 = 0;
     for (;;) {  // the reference's order: first improving candidate at the current longest
-      bool pass = false;
-      if (ok32 && lane >= k0 && len > longest) {
+      // the read16 prefilter at longest-1 from the low limit (lz4hc.c:264): both of its bytes
+      // lie inside the measured match when that reaches back to the low limit (always, for
+      // a search without look-back), so only the other candidates have to read them
+      const bool cand = ok32 && lane >= k0 && len > longest;
+      const bool sure = back == -br;
+      bool pass = cand && sure;
+      if (ballot(cand && !sure)) {
+        const bool rd = cand && !sure;
         const int a = ilow + longest - 1, q = c - br + longest - 1;
-        pass = ldb(s + a) == ldb(s + q) && ldb(s + a + 1) == ldb(s + q + 1);
+        // (a candidate that is read has q >= 0: its low limit lies inside the block)
+        const uint32_t x0 = ldb(s + (rd ? a : ip)), y0 = ldb(s + (rd ? q : ip));
+        const uint32_t x1 = ldb(s + (rd ? a + 1 : ip)), y1 = ldb(s + (rd ? q + 1 : ip));
+        pass = pass || (rd && x0 == y0 && x1 == y1);
       }
       const uint64_t m = ballot(pass);
       if (!m) break;
@@ -427,23 +451,29 @@ __device__ int hc_encode(const HcBlock &b, uintptr_t d, int &op, int oend, int &
 // Positions it cannot settle cheaply (long buckets, level-9 repetitive
 // patterns) report false and get the full search.
 __device__ __forceinline__ bool hc_sure_miss(const HcBlock &b, int p, int mflimit) {
-  if (p > mflimit) return false;
-  const uint32_t pat = ld32u(b.s + p);
-  if (b.pa && ((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24))) return false;
-  const uint32_t t = b.tr[p];
+  // every load is unconditional on a clamped address (a predicated load is waited for at
+  // once): three dependent round trips per 64 positions, not one per candidate.  A
+  // position up to mflimit has 11 block bytes behind it, so the 8-byte reads stay inside.
+  const bool in = p <= mflimit;
+  const int pc = in ? p : mflimit;
+  const uint32_t pat = ld32u_nb(b.s + pc);
+  const uint32_t t = b.tr[pc];
+  const bool rep = b.pa && ((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24));
   const int r = int(t >> 16);
   const int total = r < b.attempts ? r : b.attempts;
-  if (total == 0) return true;
-  if (total > 8) return false;
   const int top = int(t & 0xFFFFu) - 1;
   int c[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) c[j] = j < total ? int(b.sorted[top - j]) : -1;
+  for (int j = 0; j < 8; ++j) c[j] = int(b.sorted[j < total ? top - j : 0]);
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = ld32u_nb(b.s + (j < total ? c[j] : pc));
   bool miss = true;
 #pragma unroll
   for (int j = 0; j < 8; ++j)
-    if (c[j] >= 0 && ld32u(b.s + c[j]) == pat) miss = false;
-  return miss;
+    if (j < total && w[j] == pat) miss = false;
+  if (!in || rep || total > 8) return false;
+  return miss;  // (total == 0: nothing to test)
 }
 
 // LZ4HC_compress_hashChain (lz4hc.c:532-746).  Returns the compressed size or

@@ -347,8 +347,9 @@ __device__ __forceinline__ int hc_count_back(uintptr_t s, int ip, int c, int lim
   return back;
 }
 
-// LZ4HC_InsertAndGetWiderMatch, 64 chain candidates per step
-__device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int longest, int &mpos,
+// LZ4HC_InsertAndGetWiderMatch, 64 chain candidates per step; reads no further than the
+// reference does (the last positions of a block, where hc_search()'s windows would run over)
+__device__ int hc_search_edge(const HcBlock &b, int ip, int ilow, int ihigh, int longest, int &mpos,
                          int &spos) {
   const uintptr_t s = b.s;
   const int lane = b.lane;
@@ -375,6 +376,97 @@ __device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int long
       }
       len = 4 + hc_count(s, ip + 4, c + 4, ihigh) - back;
     }
+    int k0 = 0;
+    for (;;) {  // the reference's order: first improving candidate at the current longest
+      // the read16 prefilter at longest-1 from the low limit (lz4hc.c:264): both of its bytes
+      // lie inside the measured match when that reaches back to the low limit (always, for
+      // a search without look-back), so only the other candidates have to read them
+      const bool cand = ok32 && lane >= k0 && len > longest;
+      const bool sure = back == -br;
+      bool pass = cand && sure;
+      if (ballot(cand && !sure)) {
+        const bool rd = cand && !sure;
+        const int a = ilow + longest - 1, q = c - br + longest - 1;
+        // (a candidate that is read has q >= 0: its low limit lies inside the block)
+        const uint32_t x0 = ldb(s + (rd ? a : ip)), y0 = ldb(s + (rd ? q : ip));
+        const uint32_t x1 = ldb(s + (rd ? a + 1 : ip)), y1 = ldb(s + (rd ? q + 1 : ip));
+        pass = pass || (rd && x0 == y0 && x1 == y1);
+      }
+      const uint64_t m = ballot(pass);
+      if (!m) break;
+      const int k = __builtin_ctzll(m);
+      longest = __shfl(len, k);
+      mpos = __shfl(c + back, k);
+      spos = ip + __shfl(back, k);
+      k0 = k + 1;
+    }
+  }
+  return longest;
+}
+
+// 4-aligned dwords d[0..N) hold bytes from address (a & ~3): word k of the byte stream at a
+template <int N>
+__device__ __forceinline__ void hc_load_words(uintptr_t a, uint32_t w[N]) {
+  const uintptr_t base = a & ~uintptr_t(3);
+  const uint32_t sh = uint32_t(a & 3u);
+  uint32_t d[N + 1];
+#pragma unroll
+  for (int k = 0; k <= N; ++k) d[k] = *(g_cu32 *)(base + 4 * k);
+#pragma unroll
+  for (int k = 0; k < N; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+
+// LZ4HC_InsertAndGetWiderMatch, 64 chain candidates per step.  One round trip fetches a
+// candidate's 36 bytes (the MINMATCH test and the first 32 bytes of LZ4_count) and the 8
+// bytes in front of it (countBack), on clamped addresses; the source's windows are loaded
+// once, with the pattern and the table entry.  Longer matches continue from memory.
+__device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int longest, int &mpos,
+                         int &spos) {
+  if (ip + 48 > ihigh) return hc_search_edge(b, ip, ilow, ihigh, longest, mpos, spos);
+  const uintptr_t s = b.s;
+  const int lane = b.lane;
+  uint32_t sw[9], sb[2];
+  hc_load_words<9>(s + ip, sw);  // bytes ip .. ip+36 (ip + 40 < block end)
+  const uint32_t t = b.tr[ip];   // one load instead of rank -> hash -> bucket start
+  const int br = ip - ilow;
+  const bool wideback = br != 0 && ip >= 8;
+  hc_load_words<2>(s + (wideback ? ip - 8 : ip), sb);  // bytes ip-8 .. ip
+  const uint32_t pat = sw[0];
+  if (b.pa && ((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24)))
+    return hc_search_serial(b, ip, ilow, ihigh, longest, mpos, spos, pat, false);
+  const int r = int(t >> 16);
+  const int top = int(t & 0xFFFFu) - 1;  // sorted[top] = latest earlier same-hash
+  const int total = r < b.attempts ? r : b.attempts;
+  for (int c0 = 0; c0 < total; c0 += 64) {
+    const int j = c0 + lane;
+    const bool valid = j < total;
+    const int c = int(b.sorted[valid ? top - j : top]);
+    uint32_t cw[9], cb[2];
+    hc_load_words<9>(s + c, cw);  // (c < ip)
+    const bool cback = wideback && c >= 8;
+    hc_load_words<2>(s + (cback ? c - 8 : c), cb);
+    const bool ok32 = (cw[0] == pat) & valid;
+    int fwd = 32;
+#pragma unroll
+    for (int k = 8; k >= 1; --k) {
+      const uint32_t z = sw[k] ^ cw[k];
+      if (z) fwd = 4 * (k - 1) + (__builtin_ctz(z) >> 3);
+    }
+    if (ballot(ok32 && fwd == 32)) {  // (ip + 36 < ihigh, so the 32 bytes were all countable)
+      if (ok32 && fwd == 32) fwd += hc_count(s, ip + 36, c + 36, ihigh);
+    }
+    int back = 0;
+    if (br) {
+      const int lim = (ilow - ip) > -c ? (ilow - ip) : -c;  // LZ4HC_countBack (lz4hc.c:140-152)
+      const uint32_t x1 = sb[1] ^ cb[1], x0 = sb[0] ^ cb[0];
+      const int eqb = x1 ? int(__builtin_clz(x1) >> 3) : 4 + (x0 ? int(__builtin_clz(x0) >> 3) : 4);
+      back = -(eqb < -lim ? eqb : -lim);
+      const bool slow = ok32 && (cback ? (eqb == 8 && lim < -8) : true);
+      if (ballot(slow)) {
+        if (slow) back = cback ? hc_count_back(s, ip - 8, c - 8, lim + 8) - 8 : hc_count_back(s, ip, c, lim);
+      }
+    }
+    const int len = ok32 ? 4 + fwd - back : 0;
     int k0 = 0;
     for (;;) {  // the reference's order: first improving candidate at the current longest
       // the read16 prefilter at longest-1 from the low limit (lz4hc.c:264): both of its bytes
@@ -972,8 +1064,9 @@ __global__ __launch_bounds__(kHcBuildThreads) void lz4hc_build_kernel(
 // item `it` has its tables at scratch + (it - it0) * kHcScratch, built by lz4hc_build_kernel
 // for its first block (frames of more than 64 blocks: the wave builds the further ones
 // itself, in the same tables).
+// (four waves per SIMD: a 4096-item chunk is resident at once)
 template <bool OPT>
-__global__ __launch_bounds__(64) void lz4hc_compress_blocks_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void lz4hc_compress_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ out_offs, uint32_t n, int attempts, int sufficient,

@@ -17,8 +17,9 @@
 //    and the catch-up (up to 4) from registers.  The sequential loop's path over
 //    those per-lane results -- which positions are probed and inserted, the first
 //    verifying probe, catch-up, ip-2 insertion and the immediate re-test after a
-//    match (lz4.c:1084-1134) -- is then found by pointer doubling over the
-//    verified lanes (the parallel walk); windows outside the conditions under
+//    match (lz4.c:1084-1134) -- is then the orbit of the entry lane under "next
+//    verified lane behind this lane's match", hopped on the scalar unit over per-lane
+//    results (the parallel walk); windows outside the conditions under
 //    which that shortcut is exact are replayed one sequence at a time (the scalar
 //    walk).  A candidate inserted earlier in the same window is found with a
 //    hash-equality mask over the lanes.  Several sequences per window cost two
@@ -51,6 +52,12 @@
 #include "lz4_engine.h"
 #include "lz4_wave.h"
 #include "win_ring.h"
+
+#ifdef RDK_WIN_PROF
+#define RDK_PT(k) do { const uint64_t now_ = __builtin_amdgcn_s_memtime(); b.pt[k] += now_ - tprev_; tprev_ = now_; } while (0)
+#else
+#define RDK_PT(k) do { } while (0)
+#endif
 
 namespace rdk {
 
@@ -324,6 +331,9 @@ struct WinBlock : SrcRing {  // + the block's source and its LDS ring (win_ring.
   int cnt;     // probes already made in the current search
   int anchor, op;
   int mode;    // how the next window starts
+#ifdef RDK_WIN_PROF
+  uint64_t pt[8], pn;
+#endif
 };
 
 // One window of 64 positions from w0.  See the file comment; tests/sim/lz4_window_sim.cpp
@@ -331,6 +341,10 @@ struct WinBlock : SrcRing {  // + the block's source and its LDS ring (win_ring.
 __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand, lds_u16 *table,
                                            int lane) {
   const int mode = b.mode;
+#ifdef RDK_WIN_PROF
+  uint64_t tprev_ = __builtin_amdgcn_s_memtime();
+  b.pn++;
+#endif
   // ---------------------------------------------------------------- per lane
   const int i = w0 + lane;
   const bool act = i <= b.n - kLz4MFLimit;  // position + 1 <= mflimitPlusOne
@@ -342,6 +356,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
   const uint32_t seq = __builtin_amdgcn_alignbyte(xd[2], xd[1], shi);
   const uint32_t h = lz4_hash(seq);
+  RDK_PT(0);
   int tc = act ? int(table[h]) : 0;
   if (mode == W_FORCED && lane == 0) tc = forced_cand;
   // the candidate's 36 bytes: from the ring when it is that recent, else from memory
@@ -362,6 +377,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   const uint32_t shc = (uint32_t(tc) + b.sa) & 3u;
   const bool tver = act && seq == __builtin_amdgcn_alignbyte(yt[2], yt[1], shc);
   const uint64_t VT = ballot(tver);
+  RDK_PT(1);
   int len = kRegLen;
 #pragma unroll
   for (int k = 6; k >= 1; --k) {
@@ -392,6 +408,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
       }
     }
   }
+  RDK_PT(2);
   if (len > b.mlim - i) len = b.mlim - i;  // LZ4_count stops at matchlimit
   const bool sat = tver && i + len < b.mlim && (len == kMaxLen || (far && len == kRegLen));
   const uint32_t back = __builtin_amdgcn_alignbyte(xd[1], xd[0], shi);  // bytes i-4 .. i-1
@@ -440,8 +457,8 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
 
   // ------------------------------------------------------------ parallel walk
   // Matches hop from one verified lane to the next: f(m) = first verified lane at or after
-  // m + len[m]; the chosen lanes are the orbit of f from the entry, found by pointer
-  // doubling (a match is at least 4 long, so at most 16 fit in a window).  This assumes
+  // m + len[m]; the chosen lanes are the orbit of f from the entry (a match is at least 4
+  // long, so at most 16 fit in a window).  This assumes
   // every candidate is the table's (no lane of this window supplies one); that and the rare
   // shapes (length or catch-up not final, strides above 1, end of block) are checked
   // afterwards, and the scalar walk below redoes the window when a check fails.
@@ -451,38 +468,13 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
     const int tl = lane + len;
     const uint64_t fm = tl >= 64 ? 0ull : VT & (~0ull << tl);
     const int J0 = fm ? __builtin_ctzll(fm) : 64;
-    // (every lane takes part in each shuffle: a lane that is switched off reads as 0)
-    const int s1 = __shfl(J0, J0 & 63);
-    const int J1 = J0 < 64 ? s1 : 64;
-    const int s2 = __shfl(J1, J1 & 63);
-    const int J2 = J1 < 64 ? s2 : 64;
-    const int s3 = __shfl(J2, J2 & 63);
-    const int J3 = J2 < 64 ? s3 : 64;
+    // the orbit of the entry lane under J0, hop by hop on the scalar unit: one v_readlane
+    // and a handful of scalar instructions per match, a dependent chain far shorter than
+    // the cross-lane shuffles of a pointer-doubling scheme
     const uint64_t em = VT & ~bits_below(e);
-    int pos = em ? __builtin_ctzll(em) : 64;  // lane k < 16 looks up the k-th match
-    {
-      const int p0 = __shfl(J0, pos & 63);
-      if ((lane & 1) && pos < 64) pos = p0;
-      const int p1 = __shfl(J1, pos & 63);
-      if ((lane & 2) && pos < 64) pos = p1;
-      const int p2 = __shfl(J2, pos & 63);
-      if ((lane & 4) && pos < 64) pos = p2;
-      const int p3 = __shfl(J3, pos & 63);
-      if ((lane & 8) && pos < 64) pos = p3;
-    }
-    // OR of (1 << pos) over lanes 0..15: a DPP scan inside the first row
-    uint32_t blo = (lane < 16 && pos < 32) ? 1u << pos : 0u;
-    uint32_t bhi = (lane < 16 && pos >= 32 && pos < 64) ? 1u << (pos - 32) : 0u;
-#define RDK_ROW_OR(v)                                                                  \
-    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, true));      \
-    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, true));      \
-    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, true));      \
-    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, true));
-    RDK_ROW_OR(blo)
-    RDK_ROW_OR(bhi)
-#undef RDK_ROW_OR
-    const uint64_t ch = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(bhi), 15))) << 32) |
-                        uint32_t(__builtin_amdgcn_readlane(int(blo), 15));
+    uint64_t ch = 0;
+    for (int pos = em ? __builtin_ctzll(em) : 64; pos < 64; pos = __builtin_amdgcn_readlane(J0, pos))
+      ch |= 1ull << pos;
     // per lane: the end of the previous chosen match
     const uint64_t lowc = ch & ((1ull << lane) - 1ull);
     const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
@@ -528,6 +520,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
     }
   }
 
+  RDK_PT(3);
   if (!fast_done) {
   bool have = false;  // a verified match at lane x is pending
   bool post = false;  // a match just ended at ipn
@@ -631,6 +624,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   }  // !fast_done
 #undef RDK_WIN_LOOKUP
 
+  RDK_PT(4);
   // ------------------------------------------------------------ table update
   // every inserted lane; the latest position per hash wins
   if (st != W_LAST) {
@@ -639,6 +633,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
     if (ins && !later) table[h] = uint16_t(i);
     asm volatile("" ::: "memory");
   }
+  RDK_PT(5);
   // ---------------------------------------------------------------- emission
   // Each chosen lane writes its own token, literal-length bytes, literals, offset and
   // match-length bytes at a wave-prefix-sum position.  Every window runs the same store
@@ -712,6 +707,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
     b.op += int(tot);
   }
   b.anchor = anchor;
+  RDK_PT(6);
   return st;
 }
 
@@ -732,6 +728,11 @@ __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table,
   b.anchor = 0;
   b.op = 0;
   b.mode = W_SEARCH;
+#ifdef RDK_WIN_PROF
+  for (int k = 0; k < 8; ++k) b.pt[k] = 0;
+  b.pn = 0;
+  const uint64_t tstart_ = __builtin_amdgcn_s_memtime();
+#endif
   int forced = 0;
   for (;;) {
     int w0;
@@ -749,6 +750,13 @@ __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table,
     if (st == W_OVERFLOW) return 0;
     if (st == W_LAST) break;
   }
+#ifdef RDK_WIN_PROF
+  if (lane == 0 && (blockIdx.x % 509) == 0)
+    printf("WINPROF blk %u windows %llu total %llu | own %llu cand %llu ext %llu walk %llu scalar %llu table %llu emit %llu\n", blockIdx.x,
+           (unsigned long long)b.pn, (unsigned long long)(__builtin_amdgcn_s_memtime() - tstart_), (unsigned long long)b.pt[0],
+           (unsigned long long)b.pt[1], (unsigned long long)b.pt[2], (unsigned long long)b.pt[3], (unsigned long long)b.pt[4],
+           (unsigned long long)b.pt[5], (unsigned long long)b.pt[6]);
+#endif
   // last literals (lz4.c:1141-1166)
   const uint32_t last = uint32_t(n - b.anchor);
   if (b.op + int(last) + 1 + int((last + 255u - 15u) / 255u) > b.olimit) return 0;

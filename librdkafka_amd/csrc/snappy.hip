@@ -236,7 +236,7 @@ __device__ uint32_t sn_compress_fragment(uintptr_t src, uint32_t n, uintptr_t ds
 // up to 92 from the ring).  The sequential loop's path over those per-lane results -- which
 // positions are probed and inserted, the first verifying probe, the ip-1 insertion and the
 // immediate re-test behind a copy (:1071-1088) -- is the orbit of the entry lane under
-// next(m) = first verified lane >= m + len(m), found by pointer doubling (the parallel
+// next(m) = first verified lane >= m + len(m), hopped on the scalar unit (the parallel
 // walk).  The skip schedule leaves stride 1 after probe 31 of a search (skip++ >> 5 from
 // 32, :1019): the walk is cut at the first lane a search would reach with a higher probe
 // index, and sn_generic_search() continues from there probe by probe, 64 probes per step.
@@ -400,38 +400,12 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
     const int tl = lane + len;
     const uint64_t fm = tl >= 64 ? 0ull : VT & (~0ull << tl);
     const int J0 = fm ? __builtin_ctzll(fm) : 64;
-    // (every lane takes part in each shuffle: a lane that is switched off reads as 0)
-    const int s1 = __shfl(J0, J0 & 63);
-    const int J1 = J0 < 64 ? s1 : 64;
-    const int s2 = __shfl(J1, J1 & 63);
-    const int J2 = J1 < 64 ? s2 : 64;
-    const int s3 = __shfl(J2, J2 & 63);
-    const int J3 = J2 < 64 ? s3 : 64;
+    // the orbit of the entry lane under J0, hop by hop on the scalar unit (one v_readlane
+    // and a handful of scalar instructions per copy)
     const uint64_t em = VT & ~bits_below(e);
-    int pos = em ? __builtin_ctzll(em) : 64;  // lane k < 16 looks up the k-th copy
-    {
-      const int p0 = __shfl(J0, pos & 63);
-      if ((lane & 1) && pos < 64) pos = p0;
-      const int p1 = __shfl(J1, pos & 63);
-      if ((lane & 2) && pos < 64) pos = p1;
-      const int p2 = __shfl(J2, pos & 63);
-      if ((lane & 4) && pos < 64) pos = p2;
-      const int p3 = __shfl(J3, pos & 63);
-      if ((lane & 8) && pos < 64) pos = p3;
-    }
-    // OR of (1 << pos) over lanes 0..15: a DPP scan inside the first row
-    uint32_t blo = (lane < 16 && pos < 32) ? 1u << pos : 0u;
-    uint32_t bhi = (lane < 16 && pos >= 32 && pos < 64) ? 1u << (pos - 32) : 0u;
-#define RDK_ROW_OR(v)                                                                  \
-    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, true));      \
-    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, true));      \
-    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, true));      \
-    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, true));
-    RDK_ROW_OR(blo)
-    RDK_ROW_OR(bhi)
-#undef RDK_ROW_OR
-    uint64_t ch = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(bhi), 15))) << 32) |
-                  uint32_t(__builtin_amdgcn_readlane(int(blo), 15));
+    uint64_t ch = 0;
+    for (int pos = em ? __builtin_ctzll(em) : 64; pos < 64; pos = __builtin_amdgcn_readlane(J0, pos))
+      ch |= 1ull << pos;
     // per lane: the end of the previous chosen copy
     const uint64_t lowc = ch & ((1ull << lane) - 1ull);
     const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;

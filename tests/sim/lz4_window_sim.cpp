@@ -147,7 +147,8 @@ Status window(Block &b, int w0, Mode mode, int forced_cand, Mode &next_mode) {
 
   // ---- parallel walk (the kernel's fast path).  Matches hop from one verified lane to the
   // next: f(m) = first verified lane at or after m + len[m]; the chosen lanes are the orbit
-  // of f from the entry, found by pointer doubling (at most 16 matches fit in a window).
+  // of f from the entry (at most 16 matches fit in a window; computed here by doubling,
+  // in the kernel hop by hop: the same set).
   // It assumes every candidate is the table's (no lane of this window supplies one); that
   // and the rare shapes are checked afterwards, and the scalar walk below redoes the window
   // when a check fails.

@@ -4,7 +4,7 @@
 // TEST INFRASTRUCTURE.  The HIP kernel reproduces compress_fragment's greedy parse
 // (snappy.c:957-1103) in windows of 64 consecutive positions, one per lane: every lane
 // measures the match its table candidate would give, and the sequential loop's path over
-// those per-lane results is found by pointer doubling (the parallel walk), with a walk that
+// those per-lane results is an orbit over the lanes (the parallel walk), with a walk that
 // takes one copy at a time for the windows outside the conditions under which that shortcut
 // is exact.  This file is the same algorithm with the 64 lanes as arrays and the wave
 // intrinsics as loops, so the parse logic (which positions are probed and inserted, the

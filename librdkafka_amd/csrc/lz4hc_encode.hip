@@ -688,23 +688,42 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool pr
 // chain swap on) for a pattern that is not one repeated byte, so that pattern
 // analysis never redirects the walk.  64 candidates of the current chain per step.
 __device__ int hc_search_swap(const HcBlock &b, int ip, int ihigh, int longest, int &mpos,
-                              uint32_t pat) {
+                              const uint32_t sw[9], uint32_t t_first, bool wide) {
   const uintptr_t s = b.s;
   const int lane = b.lane;
+  const uint32_t pat = sw[0];
   int attempts = b.attempts;
   int q = ip, cp = 0;  // the walk follows the chain of position q = candidate + cp
+  uint32_t t = t_first;  // tr[q]
   for (;;) {
-    const uint32_t t = b.tr[q];
     const int r = int(t >> 16), top = int(t & 0xFFFFu) - 1;
     const int total = r < attempts ? r : attempts;
     bool swapped = false;
     for (int c0 = 0; c0 < total; c0 += 64) {
       const int j = c0 + lane;
-      const int m = j < total ? int(b.sorted[top - j]) - cp : -1;
-      const bool valid = m >= 0;
-      const bool ok32 = valid && ld32u(s + m) == pat;
+      const bool inq = j < total;
+      const int m = int(b.sorted[inq ? top - j : top]) - cp;  // (clamped, not predicated)
+      const bool valid = inq && m >= 0;
+      bool ok32;
       int len = 0;
-      if (ok32) len = 4 + hc_count(s, ip + 4, m + 4, ihigh);
+      if (wide) {  // the candidate's 36 bytes in one round trip (m < ip, ip + 48 <= ihigh)
+        uint32_t cw[9];
+        hc_load_words<9>(s + (valid ? m : ip), cw);
+        ok32 = valid && cw[0] == pat;
+        int fwd = 32;
+#pragma unroll
+        for (int k = 8; k >= 1; --k) {
+          const uint32_t z = sw[k] ^ cw[k];
+          if (z) fwd = 4 * (k - 1) + (__builtin_ctz(z) >> 3);
+        }
+        if (ballot(ok32 && fwd == 32)) {
+          if (ok32 && fwd == 32) fwd += hc_count(s, ip + 36, m + 36, ihigh);
+        }
+        len = ok32 ? 4 + fwd : 0;
+      } else {
+        ok32 = valid && ld32u(s + m) == pat;
+        if (ok32) len = 4 + hc_count(s, ip + 4, m + 4, ihigh);
+      }
       int k0 = 0;
       for (;;) {  // the reference's order: the next candidate that ties or beats `longest`
         bool pass = ok32 && lane >= k0 && len >= longest;
@@ -733,9 +752,10 @@ __device__ int hc_search_swap(const HcBlock &b, int ip, int ihigh, int longest, 
         k0 = k + 1;
       }
       if (swapped) break;
-      if (ballot(j < total && !valid)) return longest;  // the chain left the block: the walk ends
+      if (ballot(inq && !valid)) return longest;  // the chain left the block: the walk ends
     }
     if (!swapped || attempts <= 0) break;  // chain or attempts used up
+    t = b.tr[q];
   }
   return longest;
 }
@@ -743,12 +763,25 @@ __device__ int hc_search_swap(const HcBlock &b, int ip, int ihigh, int longest, 
 // LZ4HC_FindLongerMatch (lz4hc.c:1255-1275), favorCompressionRatio: the length
 // (0 when nothing beats min_len) and the offset
 __device__ int hc_longer(const HcBlock &b, int ip, int ihigh, int min_len, int &off) {
-  const uint32_t pat = ld32u(b.s + ip);
+  // the source's 36 bytes (the pattern first) and the table entry in one round trip; the
+  // last positions of a block, where the windows would run over its end, read as the
+  // reference does
+  const bool wide = ip + 48 <= ihigh;
+  uint32_t sw[9];
+  if (wide) {
+    hc_load_words<9>(b.s + ip, sw);
+  } else {
+#pragma unroll
+    for (int k = 1; k < 9; ++k) sw[k] = 0;
+    sw[0] = ld32u(b.s + ip);
+  }
+  const uint32_t t0 = b.tr[ip];
+  const uint32_t pat = sw[0];
   int mpos = 0, spos = ip, len;
   if (((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24)))
     len = hc_search_serial(b, ip, ip, ihigh, min_len, mpos, spos, pat, true);
   else
-    len = hc_search_swap(b, ip, ihigh, min_len, mpos, pat);
+    len = hc_search_swap(b, ip, ihigh, min_len, mpos, sw, t0, wide);
   if (len <= min_len) return 0;
   off = ip - mpos;
   return len;

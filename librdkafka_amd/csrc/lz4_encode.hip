@@ -331,10 +331,75 @@ struct WinBlock : SrcRing {  // + the block's source and its LDS ring (win_ring.
   int cnt;     // probes already made in the current search
   int anchor, op;
   int mode;    // how the next window starts
+  uint32_t q0, q1;  // the sequence queue, one entry per lane (flush_sequences)
+  int qn;           // entries queued
 #ifdef RDK_WIN_PROF
   uint64_t pt[8], pn;
 #endif
 };
+
+// Write out the queued sequences (lane q < qn holds one: literal start | literal length << 16,
+// offset | matchlength-4 << 16): token, literal-length bytes, literals, offset and
+// match-length bytes at wave-prefix-sum positions.  true: the block does not fit
+// (limitedOutput).
+__device__ __forceinline__ bool flush_sequences(WinBlock &b, int lane) {
+  const bool ch = lane < b.qn;
+  const uint32_t lstart = b.q0 & 0xFFFFu, lit = ch ? b.q0 >> 16 : 0u;
+  const uint32_t off = b.q1 & 0xFFFFu, mc = b.q1 >> 16;
+  const uint32_t lext = ext_bytes(lit);
+  const uint32_t sz = ch ? 3u + lit + lext + ext_bytes(mc) : 0u;
+  uint32_t tot;
+  const uint32_t o = wave_excl_scan(sz, tot);
+  const uint32_t tp = uint32_t(b.op) + o;  // token position in the block output
+  const uint32_t lp = tp + 1u + lext;      // first literal
+  const uint32_t fp = lp + lit;            // offset field
+  // limitedOutput, lz4.c:964 (literals) and lz4.c:1044 (match length)
+  const bool ov = ch && (int(tp + 1u + lit + (2u + 1u + kLz4LastLiterals) + lit / 255u) > b.olimit ||
+                         int(fp + 2u + (1u + kLz4LastLiterals) + (mc + 240u) / 255u) > b.olimit);
+  if (ballot(ov)) return true;
+  __builtin_amdgcn_raw_buffer_store_b8(
+      uint8_t(((lit < 15u ? lit : 15u) << 4) | (mc < 15u ? mc : 15u)), b.w, ch ? tp : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), b.w, ch ? fp : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), b.w, ch ? fp + 1u : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(mc - 15u), b.w,
+                                       (ch && mc >= 15u && mc < 270u) ? fp + 2u : kNoLoad, 0, 0);
+  // rare shapes, each behind a wave-uniform test
+  if (ballot(ch && lit >= 15u)) {
+    if (ch && lit >= 15u) put_len(b.dst + tp + 1u, lit);
+  }
+  if (ballot(ch && mc >= 270u)) {
+    if (ch && mc >= 270u) put_len(b.dst + fp + 2u, mc);
+  }
+  // up to 16 literals: one 20-byte window per lane, from the ring while it still holds them
+  const uint32_t la = (lstart + b.sa) & ~3u;
+  const bool need_win = ch && lit != 0u && lit <= kShortLit && int(la) >= b.H - int(kRingBytes);
+  if (ballot(need_win)) {
+    uint32_t wv[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      wv[k] = *(lds_u32 *)((lds_u8 *)b.ring + ((la + 4u * uint32_t(k)) & (kRingBytes - 1u)));
+    const uint32_t sh = (lstart + b.sa) & 3u;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], sh);
+#pragma unroll
+    for (uint32_t k = 0; k < kShortLit; ++k)
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), b.w,
+                                           (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
+  }
+  uint64_t longm = ballot(ch && lit != 0u && !need_win);  // long runs: the whole wave copies them
+  while (longm) {
+    const int j = __builtin_ctzll(longm);
+    longm &= longm - 1;
+    const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
+    const uint32_t jp = __builtin_amdgcn_readlane(lp, j);
+    const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
+    wave_copy_bytes(b.dst + jp, b.src + js, jl, lane);
+  }
+  b.op += int(tot);
+  b.qn = 0;
+  return false;
+}
 
 // One window of 64 positions from w0.  See the file comment; tests/sim/lz4_window_sim.cpp
 // is the same walk with the lanes as arrays.
@@ -634,77 +699,31 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
     asm volatile("" ::: "memory");
   }
   RDK_PT(5);
-  // ---------------------------------------------------------------- emission
-  // Each chosen lane writes its own token, literal-length bytes, literals, offset and
-  // match-length bytes at a wave-prefix-sum position.  Every window runs the same store
-  // instructions (parked lanes write nothing).
+  // ---------------------------------------------------------------- sequences
+  // A window holds a handful of sequences, far fewer than lanes: they are queued, one per
+  // lane of the queue registers, and written out 64 at a time (flush_sequences).
   {
     const bool ch = (chosen >> lane) & 1ull;
     const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
     const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
-    const int pend = __shfl(i + L_len, pl);  // end of the previous chosen match
+    const int pend = __shfl(i + L_len, pl);    // end of the previous chosen match
     const int prev = lowc ? pend : anchor_in;  // this sequence's anchor
-    const uint32_t lit = ch ? uint32_t(i - L_bk - prev) : 0u;
+    const uint32_t lit = uint32_t(i - L_bk - prev);
     const uint32_t mc = uint32_t(L_len + L_bk - 4);
-    const uint32_t lext = ext_bytes(lit);
-    const uint32_t sz = ch ? 3u + lit + lext + ext_bytes(mc) : 0u;
-    uint32_t tot;
-    const uint32_t o = wave_excl_scan(sz, tot);
-    const uint32_t tp = uint32_t(b.op) + o;  // token position in the block output
-    const uint32_t lp = tp + 1u + lext;      // first literal
-    const uint32_t fp = lp + lit;            // offset field
-    // limitedOutput, lz4.c:964 (literals) and lz4.c:1044 (match length)
-    const bool ov = ch && (int(tp + 1u + lit + (2u + 1u + kLz4LastLiterals) + lit / 255u) > b.olimit ||
-                           int(fp + 2u + (1u + kLz4LastLiterals) + (mc + 240u) / 255u) > b.olimit);
-    if (ballot(ov)) return W_OVERFLOW;
-    __builtin_amdgcn_raw_buffer_store_b8(
-        uint8_t(((lit < 15u ? lit : 15u) << 4) | (mc < 15u ? mc : 15u)), b.w, ch ? tp : kNoLoad, 0, 0);
-    // up to 4 literals (with the catch-up) sit in the lane's own back dword
-    const bool in_reg = ch && lit + uint32_t(L_bk) <= 4u;
-    const uint32_t first = 4u - uint32_t(L_bk) - lit;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(back >> (8u * ((first + k) & 3u))), b.w,
-                                           (in_reg && k < lit) ? lp + k : kNoLoad, 0, 0);
     const uint32_t off = uint32_t(i - L_cand);
-    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), b.w, ch ? fp : kNoLoad, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), b.w, ch ? fp + 1u : kNoLoad, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(mc - 15u), b.w,
-                                         (ch && mc >= 15u && mc < 270u) ? fp + 2u : kNoLoad, 0, 0);
-    // rare shapes, each behind a wave-uniform test
-    if (ballot(ch && lit >= 15u)) {
-      if (ch && lit >= 15u) put_len(b.dst + tp + 1u, lit);
+    const int cnt = __builtin_popcountll(chosen);
+    if (cnt) {
+      if (b.qn + cnt > 64 && flush_sequences(b, lane)) return W_OVERFLOW;
+      // chosen lane -> queue lane qn + its rank among the chosen lanes: a forward permute
+      // (scatter); the other lanes send to a lane outside the accepted range
+      const int tgt = ch ? b.qn + __builtin_popcountll(lowc) : ((b.qn + cnt) & 63);
+      const uint32_t r0 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(uint32_t(prev) | (lit << 16))));
+      const uint32_t r1 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(off | (mc << 16))));
+      const bool acc = lane >= b.qn && lane < b.qn + cnt;
+      b.q0 = acc ? r0 : b.q0;
+      b.q1 = acc ? r1 : b.q1;
+      b.qn += cnt;
     }
-    if (ballot(ch && mc >= 270u)) {
-      if (ch && mc >= 270u) put_len(b.dst + fp + 2u, mc);
-    }
-    const uint32_t lstart = uint32_t(prev);
-    const uint32_t la = (lstart + b.sa) & ~3u;
-    const bool need_win = ch && !in_reg && lit <= kShortLit && int(la) >= b.H - int(kRingBytes);
-    if (ballot(need_win)) {  // 5..16 literals: one 20-byte window per lane, from the ring
-      uint32_t wv[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k)
-        wv[k] = *(lds_u32 *)((lds_u8 *)b.ring + ((la + 4u * uint32_t(k)) & (kRingBytes - 1u)));
-      const uint32_t sh = (lstart + b.sa) & 3u;
-      uint32_t v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], sh);
-#pragma unroll
-      for (uint32_t k = 0; k < kShortLit; ++k)
-        __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), b.w,
-                                             (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
-    }
-    uint64_t longm = ballot(ch && !in_reg && !need_win);  // long runs: the whole wave copies them
-    while (longm) {
-      const int j = __builtin_ctzll(longm);
-      longm &= longm - 1;
-      const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
-      const uint32_t jp = __builtin_amdgcn_readlane(lp, j);
-      const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
-      wave_copy_bytes(b.dst + jp, b.src + js, jl, lane);
-    }
-    b.op += int(tot);
   }
   b.anchor = anchor;
   RDK_PT(6);
@@ -728,6 +747,8 @@ __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table,
   b.anchor = 0;
   b.op = 0;
   b.mode = W_SEARCH;
+  b.q0 = b.q1 = 0;
+  b.qn = 0;
 #ifdef RDK_WIN_PROF
   for (int k = 0; k < 8; ++k) b.pt[k] = 0;
   b.pn = 0;
@@ -750,6 +771,7 @@ __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table,
     if (st == W_OVERFLOW) return 0;
     if (st == W_LAST) break;
   }
+  if (flush_sequences(b, lane)) return 0;
 #ifdef RDK_WIN_PROF
   if (lane == 0 && (blockIdx.x % 509) == 0)
     printf("WINPROF blk %u windows %llu total %llu | own %llu cand %llu ext %llu walk %llu scalar %llu table %llu emit %llu\n", blockIdx.x,

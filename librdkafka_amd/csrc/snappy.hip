@@ -261,6 +261,8 @@ struct SnFrag : SrcRing {  // + the fragment's source and its LDS ring (win_ring
   int cnt;         // probes already made in the current search
   int anchor, op;  // next_emit, bytes written
   int mode;        // how the next window starts
+  uint32_t q0, q1;  // the element queue, one copy per lane (sn_flush_elements)
+  int qn;           // copies queued
 };
 
 // The search loop of :1015-1031 from probe index `cbase` at position `fwd`, 64 probes per
@@ -311,6 +313,73 @@ __device__ __forceinline__ uint32_t sn_copy_size(uint32_t len, uint32_t off) {
   uint32_t rem = len - (k64 << 6), o = 3u * k64;
   if (rem > 64u) { o += 3u; rem -= 60u; }
   return o + ((rem < 12u && off < 2048u) ? 2u : 3u);
+}
+
+// Write out the queued copies (lane q < qn holds one: literal start | literal length << 16,
+// offset | copy length << 16; a copy of a fragment is shorter than 65536 bytes): the literal
+// element in front of the copy (tag, length bytes, literal bytes) and the copy element(s) at
+// wave-prefix-sum positions.
+__device__ __forceinline__ void sn_flush_elements(SnFrag &b, int lane) {
+  const bool ch = lane < b.qn;
+  const uint32_t lstart = b.q0 & 0xFFFFu, lit = ch ? b.q0 >> 16 : 0u;
+  const uint32_t off = b.q1 & 0xFFFFu, ml = b.q1 >> 16;
+  const uint32_t ln = lit - 1u;
+  const uint32_t lhdr = lit == 0u ? 0u : ln < 60u ? 1u : ln < 256u ? 2u : 3u;  // emit_literal (:652)
+  const uint32_t sz = ch ? lhdr + lit + sn_copy_size(ml, off) : 0u;
+  uint32_t tot;
+  const uint32_t tp = uint32_t(b.op) + wave_excl_scan(sz, tot);  // the literal tag
+  const uint32_t lp = tp + lhdr;                                   // first literal byte
+  const uint32_t cp = lp + lit;                                    // the copy element
+  const bool haslit = ch && lit != 0u;
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(ln < 60u ? ln << 2 : (58u + lhdr) << 2), b.w,
+                                       haslit ? tp : kNoLoad, 0, 0);
+  if (ballot(haslit && lhdr > 1u)) {  // literals of more than 60 bytes: length bytes
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(ln), b.w, (haslit && lhdr > 1u) ? tp + 1u : kNoLoad, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(ln >> 8), b.w, (haslit && lhdr > 2u) ? tp + 2u : kNoLoad, 0, 0);
+  }
+  // the copy element (emit_copy_less_than64, :697); copies of more than 64 bytes below
+  const bool one = ch && ml <= 64u;
+  const bool c2 = ml < 12u && off < 2048u;
+  __builtin_amdgcn_raw_buffer_store_b8(
+      uint8_t(c2 ? 1u + ((ml - 4u) << 2) + ((off >> 8) << 5) : 2u + ((ml - 1u) << 2)), b.w,
+      one ? cp : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), b.w, one ? cp + 1u : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), b.w, (one && !c2) ? cp + 2u : kNoLoad, 0, 0);
+  uint64_t bigm = ballot(ch && ml > 64u);  // rare: the whole wave writes the elements (:718)
+  while (bigm) {
+    const int j = __builtin_ctzll(bigm);
+    bigm &= bigm - 1;
+    sn_emit_copy(b.dst + __builtin_amdgcn_readlane(cp, j), __builtin_amdgcn_readlane(off, j),
+                 __builtin_amdgcn_readlane(ml, j), lane);
+  }
+  // up to 16 literals: one 20-byte window per lane, from the ring while it still holds them
+  const uint32_t la = (lstart + b.sa) & ~3u;
+  const bool need_win = haslit && lit <= kSnShortLit && int(la) >= b.H - int(kRingBytes);
+  if (ballot(need_win)) {
+    uint32_t wv[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      wv[k] = *(ring_lds_u32 *)((ring_lds_u8 *)b.ring + ((la + 4u * uint32_t(k)) & (kRingBytes - 1u)));
+    const uint32_t sh = (lstart + b.sa) & 3u;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], sh);
+#pragma unroll
+    for (uint32_t k = 0; k < kSnShortLit; ++k)
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), b.w,
+                                           (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
+  }
+  uint64_t longm = ballot(haslit && !need_win);  // long runs: the whole wave copies them
+  while (longm) {
+    const int j = __builtin_ctzll(longm);
+    longm &= longm - 1;
+    const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
+    const uint32_t jp = __builtin_amdgcn_readlane(lp, j);
+    const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
+    wave_copy_bytes(b.dst + jp, b.src + js, jl, lane);
+  }
+  b.op += int(tot);
+  b.qn = 0;
 }
 
 __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand, sn_lds_u16 *table,
@@ -377,7 +446,6 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
   }
   if (len > b.n - i) len = b.n - i;  // find_match_length stops at the end of the input (:823)
   const bool sat = tver && i + len < b.n && (len == kSnMaxLen || (far && len == kSnRegLen));
-  const uint32_t back = __builtin_amdgcn_alignbyte(xd[1], xd[0], shi);  // bytes i-4 .. i-1
   const int NA = ~ACT ? __builtin_ctzll(~ACT) : 64;  // first lane that may not be probed
 
   // one readlane per copy fetches the lane's candidate, match length and `sat`
@@ -577,81 +645,30 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
     if (ins && !later) table[h] = uint16_t(i);
     asm volatile("" ::: "memory");
   }
-  // ---------------------------------------------------------------- emission
-  // Each chosen lane writes its own literal element (tag, literal bytes) and copy element
-  // at a wave-prefix-sum position.  Every window runs the same store instructions (parked
-  // lanes write nothing).
+  // ----------------------------------------------------------------- elements
+  // A window holds a handful of copies, far fewer than lanes: they are queued, one per lane
+  // of the queue registers, and written out 64 at a time (sn_flush_elements).
   {
     const bool ch = (chosen >> lane) & 1ull;
     const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
     const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
     const int pend = __shfl(i + L_len, pl);    // end of the previous chosen copy
     const int prev = lowc ? pend : anchor_in;  // where this copy's literal starts
-    const uint32_t lit = ch ? uint32_t(i - prev) : 0u;
+    const uint32_t lit = uint32_t(i - prev);
     const uint32_t off = uint32_t(i - L_cand), ml = uint32_t(L_len);
-    const uint32_t ln = lit - 1u;
-    const uint32_t lhdr = lit == 0u ? 0u : ln < 60u ? 1u : ln < 256u ? 2u : 3u;  // emit_literal (:652)
-    const uint32_t sz = ch ? lhdr + lit + sn_copy_size(ml, off) : 0u;
-    uint32_t tot;
-    const uint32_t tp = uint32_t(b.op) + wave_excl_scan(sz, tot);  // the literal tag
-    const uint32_t lp = tp + lhdr;                                   // first literal byte
-    const uint32_t cp = lp + lit;                                    // the copy element
-    const bool haslit = ch && lit != 0u;
-    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(ln < 60u ? ln << 2 : (58u + lhdr) << 2), b.w,
-                                         haslit ? tp : kNoLoad, 0, 0);
-    if (ballot(haslit && lhdr > 1u)) {  // literals of more than 60 bytes: length bytes
-      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(ln), b.w, (haslit && lhdr > 1u) ? tp + 1u : kNoLoad, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(ln >> 8), b.w, (haslit && lhdr > 2u) ? tp + 2u : kNoLoad, 0, 0);
+    const int cnt = __builtin_popcountll(chosen);
+    if (cnt) {
+      if (b.qn + cnt > 64) sn_flush_elements(b, lane);
+      // chosen lane -> queue lane qn + its rank among the chosen lanes: a forward permute
+      // (scatter); the other lanes send to a lane outside the accepted range
+      const int tgt = ch ? b.qn + __builtin_popcountll(lowc) : ((b.qn + cnt) & 63);
+      const uint32_t r0 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(uint32_t(prev) | (lit << 16))));
+      const uint32_t r1 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(off | (ml << 16))));
+      const bool acc = lane >= b.qn && lane < b.qn + cnt;
+      b.q0 = acc ? r0 : b.q0;
+      b.q1 = acc ? r1 : b.q1;
+      b.qn += cnt;
     }
-    // up to 4 literals sit in the lane's own back dword
-    const bool in_reg = haslit && lit <= 4u;
-    const uint32_t first = 4u - lit;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(back >> (8u * ((first + k) & 3u))), b.w,
-                                           (in_reg && k < lit) ? lp + k : kNoLoad, 0, 0);
-    // the copy element (emit_copy_less_than64, :697); copies of more than 64 bytes below
-    const bool one = ch && ml <= 64u;
-    const bool c2 = ml < 12u && off < 2048u;
-    __builtin_amdgcn_raw_buffer_store_b8(
-        uint8_t(c2 ? 1u + ((ml - 4u) << 2) + ((off >> 8) << 5) : 2u + ((ml - 1u) << 2)), b.w,
-        one ? cp : kNoLoad, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), b.w, one ? cp + 1u : kNoLoad, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), b.w, (one && !c2) ? cp + 2u : kNoLoad, 0, 0);
-    uint64_t bigm = ballot(ch && ml > 64u);  // rare: the whole wave writes the elements (:718)
-    while (bigm) {
-      const int j = __builtin_ctzll(bigm);
-      bigm &= bigm - 1;
-      sn_emit_copy(b.dst + __builtin_amdgcn_readlane(cp, j), __builtin_amdgcn_readlane(off, j),
-                   __builtin_amdgcn_readlane(ml, j), lane);
-    }
-    const uint32_t lstart = uint32_t(prev);
-    const uint32_t la = (lstart + b.sa) & ~3u;
-    const bool need_win = haslit && !in_reg && lit <= kSnShortLit && int(la) >= b.H - int(kRingBytes);
-    if (ballot(need_win)) {  // 5..16 literals: one 20-byte window per lane, from the ring
-      uint32_t wv[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k)
-        wv[k] = *(ring_lds_u32 *)((ring_lds_u8 *)b.ring + ((la + 4u * uint32_t(k)) & (kRingBytes - 1u)));
-      const uint32_t sh = (lstart + b.sa) & 3u;
-      uint32_t v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], sh);
-#pragma unroll
-      for (uint32_t k = 0; k < kSnShortLit; ++k)
-        __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), b.w,
-                                             (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
-    }
-    uint64_t longm = ballot(haslit && !in_reg && !need_win);  // long runs: the whole wave copies them
-    while (longm) {
-      const int j = __builtin_ctzll(longm);
-      longm &= longm - 1;
-      const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
-      const uint32_t jp = __builtin_amdgcn_readlane(lp, j);
-      const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
-      wave_copy_bytes(b.dst + jp, b.src + js, jl, lane);
-    }
-    b.op += int(tot);
   }
   b.anchor = anchor;
   return st;
@@ -673,6 +690,8 @@ __device__ uint32_t sn_window_fragment(uintptr_t src, uint32_t n, uintptr_t dst,
   b.anchor = 0;
   b.op = 0;
   b.mode = SN_SEARCH;
+  b.q0 = b.q1 = 0;
+  b.qn = 0;
   if (n >= 15u) {
     int forced = 0;
     for (;;) {
@@ -689,6 +708,7 @@ __device__ uint32_t sn_window_fragment(uintptr_t src, uint32_t n, uintptr_t dst,
       }
       if (sn_window_step(b, w0, forced, table, lane) == SN_LAST) break;
     }
+    sn_flush_elements(b, lane);
   }
   uint32_t op = uint32_t(b.op);
   if (uint32_t(b.anchor) < n)  // emit_remainder (:1097)

@@ -69,6 +69,8 @@ struct BlockCtx {
   int n, mfl, mlim, olimit;
   int p;               // parse position == anchor (end of the last match)
   int op;              // output bytes written
+  uint32_t q0, q1;     // the sequence queue, one entry per lane (flush_sequences)
+  int qn;              // entries queued
 };
 
 // Per round the lane's own 36-byte window (Win, loaded three rounds ahead),
@@ -103,6 +105,64 @@ __device__ __forceinline__ void round_lookup(const BlockCtx &b, const Win &x, Ca
   if (act) table[h] = uint16_t(i);
   y.c = (act && i >= b.p && c < i) ? c : -1;
   load9(b.r, y.c >= 0 ? ((uint32_t(c) + b.sa) & ~3u) : kNoLoad, y.t);
+}
+
+// Write out the queued sequences (lane q < qn holds one: literal start | literal length << 16,
+// offset | matchlength-4 << 16): every lane writes its own token, literals, offset and length
+// bytes at a wave-prefix-sum position.  false: the block does not fit in olimit bytes.
+__device__ __forceinline__ bool flush_sequences(BlockCtx &b, int lane) {
+  const bool ch = lane < b.qn;
+  const uint32_t lstart = b.q0 & 0xFFFFu, lit = ch ? b.q0 >> 16 : 0u;
+  const uint32_t off = b.q1 & 0xFFFFu, mc = b.q1 >> 16;
+  const uint32_t lext = ext_bytes(lit);
+  const uint32_t sz = ch ? 3u + lit + lext + ext_bytes(mc) : 0u;
+  uint32_t tot;
+  const uint32_t o = wave_excl_scan(sz, tot);
+  // keep room for the shortest possible last-literals token (lz4.c:1146)
+  if (b.op + int(tot) + 1 > b.olimit) return false;
+  const uint32_t tp = uint32_t(b.op) + o;  // token position in the block output
+  const uint32_t lp = tp + 1u + lext;      // first literal
+  const uint32_t fp = lp + lit;            // offset field
+  __builtin_amdgcn_raw_buffer_store_b8(
+      uint8_t(((lit < 15u ? lit : 15u) << 4) | (mc < 15u ? mc : 15u)), b.w, ch ? tp : kNoLoad, 0, 0);
+  // offset (LE16) and a single match-length byte (15 <= mc < 270)
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), b.w, ch ? fp : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), b.w, ch ? fp + 1u : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(mc - 15u), b.w,
+                                       (ch && mc >= 15u && mc < 270u) ? fp + 2u : kNoLoad, 0, 0);
+  // rare shapes, each behind a wave-uniform test
+  if (ballot(ch && lit >= 15u)) {  // literal length bytes: 255-runs + remainder
+    if (ch && lit >= 15u) put_len(b.dst + tp + 1u, lit);
+  }
+  if (ballot(ch && mc >= 270u)) {
+    if (ch && mc >= 270u) put_len(b.dst + fp + 2u, mc);
+  }
+  const bool need_win = ch && lit != 0u && lit <= kShortLit;
+  if (ballot(need_win)) {  // up to 16 literals: one 20-byte window per lane
+    uint32_t w[5];
+    load5(b.r, need_win ? ((lstart + b.sa) & ~3u) : kNoLoad, w);
+    const uint32_t sh = (lstart + b.sa) & 3u;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+#pragma unroll
+    for (uint32_t k = 0; k < kShortLit; ++k)
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), b.w,
+                                           (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
+  }
+  // long literal runs: the whole wave copies them one at a time
+  uint64_t longm = ballot(ch && lit > kShortLit);
+  while (longm) {
+    const int j = __builtin_ctzll(longm);
+    longm &= longm - 1;
+    const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
+    const uint32_t jp = __builtin_amdgcn_readlane(lp, j);
+    const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
+    wave_copy_bytes(b.dst + jp, b.src + js, jl, lane);
+  }
+  b.op += int(tot);
+  b.qn = 0;
+  return true;
 }
 
 // Measure the round's matches (windows arrived), walk the greedy parse over
@@ -162,66 +222,25 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
                       __builtin_amdgcn_alignbyte(y.t[1], y.t[0], shc);
   int bk = xb ? int(__builtin_clz(xb) >> 3) : 4;  // catch-up bytes (lz4.c:957)
   bk = min(bk, min(lane - prev, y.c));            // literals only, inside the block
-  const uint32_t lit = ch ? uint32_t(lane - bk - prev) : 0u;
-  const uint32_t ml = uint32_t(len + bk);
-  const uint32_t mc = ml - 4u;
-  const uint32_t lext = ext_bytes(lit);
-  const uint32_t sz = ch ? 3u + lit + lext + ext_bytes(mc) : 0u;
-  uint32_t tot;
-  const uint32_t o = wave_excl_scan(sz, tot);
-  // keep room for the shortest possible last-literals token (lz4.c:1146)
-  if (b.op + int(tot) + 1 > b.olimit) return false;
-  const uint32_t lstart = uint32_t(R + prev);    // absolute literal start
-  const uint32_t tp = uint32_t(b.op) + o;        // token position in the block output
-  const uint32_t lp = tp + 1u + lext;            // first literal
-  const uint32_t fp = lp + lit;                  // offset field
-  __builtin_amdgcn_raw_buffer_store_b8(
-      uint8_t(((lit < 15u ? lit : 15u) << 4) | (mc < 15u ? mc : 15u)), b.w, ch ? tp : kNoLoad, 0, 0);
-  // up to 4 literals (with the catch-up) sit in the lane's own back dword
-  const bool in_reg = ch && lit + uint32_t(bk) <= 4u;
-  const uint32_t back = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi);
-  const uint32_t first = 4u - uint32_t(bk) - lit;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; ++k)
-    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(back >> (8u * ((first + k) & 3u))), b.w,
-                                         (in_reg && k < lit) ? lp + k : kNoLoad, 0, 0);
-  // offset (LE16) and a single match-length byte (15 <= mc < 270)
+  const uint32_t lit = uint32_t(lane - bk - prev);
+  const uint32_t mc = uint32_t(len + bk) - 4u;
   const uint32_t off = uint32_t(i - y.c);
-  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), b.w, ch ? fp : kNoLoad, 0, 0);
-  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), b.w, ch ? fp + 1u : kNoLoad, 0, 0);
-  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(mc - 15u), b.w,
-                                       (ch && mc >= 15u && mc < 270u) ? fp + 2u : kNoLoad, 0, 0);
-  // rare shapes, each behind a wave-uniform test
-  if (ballot(ch && lit >= 15u)) {  // literal length bytes: 255-runs + remainder
-    if (ch && lit >= 15u) put_len(b.dst + tp + 1u, lit);
+  const uint32_t lstart = uint32_t(R + prev);  // absolute literal start
+  // A round holds a handful of sequences, far fewer than lanes: they are queued, one per
+  // lane of the queue registers, and written out 64 at a time (flush_sequences).
+  const int cnt = __builtin_popcountll(chosen);
+  if (cnt) {
+    if (b.qn + cnt > 64 && !flush_sequences(b, lane)) return false;
+    // chosen lane -> queue lane qn + its rank among the chosen lanes: a forward permute
+    // (scatter); the other lanes send to a lane outside the accepted range
+    const int tgt = ch ? b.qn + __builtin_popcountll(below) : ((b.qn + cnt) & 63);
+    const uint32_t r0 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(lstart | (lit << 16))));
+    const uint32_t r1 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(off | (mc << 16))));
+    const bool acc = lane >= b.qn && lane < b.qn + cnt;
+    b.q0 = acc ? r0 : b.q0;
+    b.q1 = acc ? r1 : b.q1;
+    b.qn += cnt;
   }
-  if (ballot(ch && mc >= 270u)) {
-    if (ch && mc >= 270u) put_len(b.dst + fp + 2u, mc);
-  }
-  const bool need_win = ch && !in_reg && lit <= kShortLit;
-  if (ballot(need_win)) {  // 5..16 literals: one 20-byte window per lane
-    uint32_t w[5];
-    load5(b.r, need_win ? ((lstart + b.sa) & ~3u) : kNoLoad, w);
-    const uint32_t sh = (lstart + b.sa) & 3u;
-    uint32_t v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-#pragma unroll
-    for (uint32_t k = 0; k < kShortLit; ++k)
-      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), b.w,
-                                           (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
-  }
-  // long literal runs: the whole wave copies them one at a time
-  uint64_t longm = ballot(ch && lit > kShortLit);
-  while (longm) {
-    const int j = __builtin_ctzll(longm);
-    longm &= longm - 1;
-    const uint32_t jl = __builtin_amdgcn_readlane(lit, j);
-    const uint32_t jp = __builtin_amdgcn_readlane(lp, j);
-    const uint32_t js = __builtin_amdgcn_readlane(lstart, j);
-    wave_copy_bytes(b.dst + jp, b.src + js, jl, lane);
-  }
-  b.op += int(tot);
   return true;
 }
 
@@ -253,6 +272,8 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
   b.mlim = n - kLz4LastLiterals;  // matchlimit (lz4.c:822)
   b.olimit = n - 1;               // LZ4F_makeBlock dstCapacity
   b.p = b.op = 0;
+  b.q0 = b.q1 = 0;
+  b.qn = 0;
 
   Win W0, W1, W2, W3;
   Cand C0, C1;
@@ -269,6 +290,7 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
     if (R + 192 > b.mfl) break;
     if (!round_step(b, W3, W0, W2, C1, C0, R + 192, table, lane)) return 0;
   }
+  if (!flush_sequences(b, lane)) return 0;
   // last literals (lz4.c:1141-1166)
   const uint32_t last = uint32_t(n - b.p);
   if (b.op + 1 + int(ext_bytes(last)) + int(last) > b.olimit) return 0;

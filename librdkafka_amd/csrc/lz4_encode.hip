@@ -528,6 +528,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   // shapes (length or catch-up not final, strides above 1, end of block) are checked
   // afterwards, and the scalar walk below redoes the window when a check fails.
   bool fast_done = false;
+  int seq_prev = 0;  // per lane: the anchor of a sequence that starts here
   if (NA == 64 && mode != W_FORCED) {
     const int e = mode == W_POSTMATCH ? 2 : 0;
     const int tl = lane + len;
@@ -562,6 +563,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
     const int x1 = ch ? __builtin_ctzll(ch) : 63;
     if (!ballot(bad) && !(mode == W_SEARCH && b.cnt + x1 > 64)) {
       fast_done = true;
+      seq_prev = prev;
       INS = ins;
       chosen = ch;
       L_cand = tc;
@@ -705,9 +707,12 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   {
     const bool ch = (chosen >> lane) & 1ull;
     const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
-    const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
-    const int pend = __shfl(i + L_len, pl);    // end of the previous chosen match
-    const int prev = lowc ? pend : anchor_in;  // this sequence's anchor
+    int prev = seq_prev;  // this sequence's anchor (the parallel walk has it already)
+    if (!fast_done) {
+      const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
+      const int pend = __shfl(i + L_len, pl);  // end of the previous chosen match
+      prev = lowc ? pend : anchor_in;
+    }
     const uint32_t lit = uint32_t(i - L_bk - prev);
     const uint32_t mc = uint32_t(L_len + L_bk - 4);
     const uint32_t off = uint32_t(i - L_cand);

@@ -463,6 +463,7 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
 
   // ------------------------------------------------------------ parallel walk
   bool fast_done = false;
+  int seq_prev = 0;  // per lane: where the literal of a copy that starts here begins
   if (NA == 64) {
     const int e = mode == SN_POSTMATCH ? 1 : 0;
     const int tl = lane + len;
@@ -499,6 +500,7 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
                                   (((Mv >> lane) & 1ull) && (eq & ins & ((1ull << lane) - 1ull))));
     if (!ballot(bad)) {
       fast_done = true;
+      seq_prev = lowc ? pend : anchor_in;
       INS = ins;
       chosen = ch;
       L_cand = tc;
@@ -651,9 +653,12 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
   {
     const bool ch = (chosen >> lane) & 1ull;
     const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
-    const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
-    const int pend = __shfl(i + L_len, pl);    // end of the previous chosen copy
-    const int prev = lowc ? pend : anchor_in;  // where this copy's literal starts
+    int prev = seq_prev;  // where this copy's literal starts (the parallel walk has it already)
+    if (!fast_done) {
+      const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
+      const int pend = __shfl(i + L_len, pl);  // end of the previous chosen copy
+      prev = lowc ? pend : anchor_in;
+    }
     const uint32_t lit = uint32_t(i - prev);
     const uint32_t off = uint32_t(i - L_cand), ml = uint32_t(L_len);
     const int cnt = __builtin_popcountll(chosen);

@@ -869,8 +869,10 @@ __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
 // slid down from their slots (raw blocks copied from the input), end mark.
 // FIN: the frame sits 61 bytes into a MsgVersion 2 batch slot and the workgroup also
 // finishes the batch (see FuseCrc): codec choice, header, CRC32C from the block registers.
+constexpr uint32_t kAsmThreads = 1024;  // 16 KiB per read-then-write step of the slide
+
 template <bool FIN>
-__global__ __launch_bounds__(256) void lz4f_assemble_kernel(
+__global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
     uint32_t *__restrict__ out_lens, uint32_t n, FuseCrc fuse) {
@@ -880,7 +882,7 @@ __global__ __launch_bounds__(256) void lz4f_assemble_kernel(
   __shared__ uint32_t s_term[FIN ? 65 : 1];
   const int t = threadIdx.x;
   if (FIN) {
-    t0_mem[t] = fuse.t0[t];
+    if (t < 256) t0_mem[t] = fuse.t0[t];
     __syncthreads();
   }
   crcw_lds_u32 *t0 = (crcw_lds_u32 *)t0_mem;
@@ -903,17 +905,17 @@ __global__ __launch_bounds__(256) void lz4f_assemble_kernel(
       const uintptr_t from = raw ? ib + uint64_t(k) * kLz4Block : slot + 4u;
       const uintptr_t to = ob + pos + 4u;
       if (from != to) {
-        for (uint32_t base = 0; base < sz; base += 256u * 16u) {
+        for (uint32_t base = 0; base < sz; base += kAsmThreads * 16u) {
           uint32_t v[16];
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
-            const uint32_t i = base + uint32_t(t) + 256u * j;
-            v[j] = i < sz ? ldb(from + i) : 0u;
+            const uint32_t i = base + uint32_t(t) + kAsmThreads * j;
+            v[j] = ldb(from + (i < sz ? i : sz - 1u));  // (clamped, not predicated)
           }
           __syncthreads();  // chunk fully read before any lane writes (dst < src)
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
-            const uint32_t i = base + uint32_t(t) + 256u * j;
+            const uint32_t i = base + uint32_t(t) + kAsmThreads * j;
             if (i < sz) stb(to + i, v[j]);
           }
           __syncthreads();
@@ -941,7 +943,7 @@ __global__ __launch_bounds__(256) void lz4f_assemble_kernel(
       const uint32_t payload = compressed ? flen : len;
       __syncthreads();                                    // the frame is complete
       if (!compressed)                                    // keep the records plain
-        for (uint32_t k = t; k < len; k += 256u) stb(ob + k, ldb(ib + k));
+        for (uint32_t k = t; k < len; k += kAsmThreads) stb(ob + k, ldb(ib + k));
       if (uint32_t(t) < kHdr) {
         uint32_t v = ldb(hdr + uint32_t(t));
         const uint32_t length = kHdr + payload - 12u;
@@ -1025,10 +1027,10 @@ void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const 
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, hipStream_t s, const FuseCrc *fuse) {
   if (fuse)
-    hipLaunchKernelGGL(lz4f_assemble_kernel<true>, dim3(n < 8192u ? n : 8192u), dim3(256), 0, s,
+    hipLaunchKernelGGL(lz4f_assemble_kernel<true>, dim3(n < 8192u ? n : 8192u), dim3(kAsmThreads), 0, s,
                        d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, *fuse);
   else
-    hipLaunchKernelGGL(lz4f_assemble_kernel<false>, dim3(n < 8192u ? n : 8192u), dim3(256), 0, s,
+    hipLaunchKernelGGL(lz4f_assemble_kernel<false>, dim3(n < 8192u ? n : 8192u), dim3(kAsmThreads), 0, s,
                        d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, FuseCrc());
 }
 

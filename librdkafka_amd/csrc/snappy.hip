@@ -760,7 +760,9 @@ __global__ __launch_bounds__(64) void snappy_compress_fragments_kernel(
 
 // One workgroup per stream: the varint32 of the input length (varint_encode32, snappy.c:297),
 // then the fragments slid together (destination always below source).
-__global__ __launch_bounds__(256) void snappy_assemble_kernel(
+constexpr uint32_t kSnAsmThreads = 1024;  // 16 KiB per read-then-write step of the slide
+
+__global__ __launch_bounds__(kSnAsmThreads) void snappy_assemble_kernel(
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
     uint32_t *__restrict__ out_lens, uint32_t n) {
   const int t = threadIdx.x;
@@ -776,17 +778,17 @@ __global__ __launch_bounds__(256) void snappy_assemble_kernel(
       const uint32_t sz = ldb(slot) | (ldb(slot + 1) << 8) | (ldb(slot + 2) << 16) | (ldb(slot + 3) << 24);
       __syncthreads();  // everyone has read the size word before it may be overwritten
       const uintptr_t from = slot + 4u, to = ob + pos;
-      for (uint32_t base = 0; base < sz; base += 256u * 16u) {
+      for (uint32_t base = 0; base < sz; base += kSnAsmThreads * 16u) {
         uint32_t v[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const uint32_t i = base + uint32_t(t) + 256u * j;
-          v[j] = i < sz ? ldb(from + i) : 0u;
+          const uint32_t i = base + uint32_t(t) + kSnAsmThreads * j;
+          v[j] = ldb(from + (i < sz ? i : sz - 1u));  // (clamped, not predicated)
         }
         __syncthreads();  // chunk fully read before any lane writes (dst < src)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const uint32_t i = base + uint32_t(t) + 256u * j;
+          const uint32_t i = base + uint32_t(t) + kSnAsmThreads * j;
           if (i < sz) stb(to + i, v[j]);
         }
         __syncthreads();
@@ -1092,7 +1094,7 @@ int snappy_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const
   else
     hipLaunchKernelGGL(snappy_compress_fragments_kernel<true>, dim3(grid), dim3(64), 0, s, d_in,
                        d_in_offs, d_in_lens, d_out, d_out_offs, n);
-  hipLaunchKernelGGL(snappy_assemble_kernel, dim3(n < 4096u ? n : 4096u), dim3(256), 0, s, d_in_lens,
+  hipLaunchKernelGGL(snappy_assemble_kernel, dim3(n < 4096u ? n : 4096u), dim3(kSnAsmThreads), 0, s, d_in_lens,
                      d_out, d_out_offs, d_out_lens, n);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;

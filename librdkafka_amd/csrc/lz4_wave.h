@@ -59,6 +59,19 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t &total) 
   return uint32_t(x) - v;
 }
 
+// exclusive running maximum over the wave of non-negative values (lane 0 gets 0): DPP row
+// shifts and row broadcasts, then one wave shift
+__device__ __forceinline__ int wave_excl_max(int v) {
+  int x = v;
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true));   // row_shr:1
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true));   // row_shr:2
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true));   // row_shr:4
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true));   // row_shr:8
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return __builtin_amdgcn_update_dpp(0, x, 0x138, 0xf, 0xf, true);        // wave_shr:1
+}
+
 // equal bytes a[i]==b[i] for i in [0, limit), 64 per wave step
 __device__ __forceinline__ int wave_count_fwd(uintptr_t a, uintptr_t b, int limit, int lane) {
   int cnt = 0;

@@ -400,17 +400,17 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
   const uint32_t ac = (uint32_t(tc) + b.sa) & ~3u;
   const bool far = act && int(ac) - 4 < b.H - int(kRingBytes);
   ring_load9(b, ac, yt);
-  if (ballot(far)) {
-    uint32_t g[9];
-    load9(b.r, far ? ac : kNoLoad, g);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) yt[k] = far ? g[k] : yt[k];
-  }
+  // (issued for every window -- parked lanes touch no memory -- and consumed behind the
+  // hash comparison below, which then runs while the gather is in flight)
+  uint32_t g[9];
+  load9(b.r, far ? ac : kNoLoad, g);
   // lanes with the same hash (the candidate may be a position inserted in this window)
   const uint64_t ACT = ballot(act);
   uint64_t eq = same_value_lanes<14>(h, ACT);
   if (!act) eq = 0;
   const uint64_t DUP = ballot((eq & ((1ull << lane) - 1ull)) != 0);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) yt[k] = far ? g[k] : yt[k];
   const uint32_t shc = (uint32_t(tc) + b.sa) & 3u;
   const bool tver = act && seq == __builtin_amdgcn_alignbyte(yt[2], yt[1], shc);
   const uint64_t VT = ballot(tver);
@@ -475,10 +475,10 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
     uint64_t ch = 0;
     for (int pos = em ? __builtin_ctzll(em) : 64; pos < 64; pos = __builtin_amdgcn_readlane(J0, pos))
       ch |= 1ull << pos;
-    // per lane: the end of the previous chosen copy
-    const uint64_t lowc = ch & ((1ull << lane) - 1ull);
-    const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
-    const int pend = __shfl(i + len, pl);
+    // per lane: the end of the previous chosen copy (0: none).  Chosen copies do not
+    // overlap, so their ends grow with the lane: a running maximum, shifted by one lane
+    const int pend = wave_excl_max(((ch >> lane) & 1ull) ? i + len : 0);
+    const bool lowc = pend != 0;
     const bool interior = lowc && pend > i;
     const uint64_t Mv = ballot(lane >= e && !interior);
     uint64_t Tm = ballot(lowc && pend == i);

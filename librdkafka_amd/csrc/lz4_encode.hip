@@ -561,6 +561,12 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
     const bool bad = (isch && ((bkr == kRegBack && blim > kRegBack) || sat || i + len >= b.mfl1)) ||
                      (((Mv >> lane) & 1ull) && (eq & ins & ((1ull << lane) - 1ull)));
     const int x1 = ch ? __builtin_ctzll(ch) : 63;
+#ifdef RDK_WIN_PROF
+    if (ballot(isch && (bkr == kRegBack && blim > kRegBack))) b.pt[7] += 1;
+    if (ballot(isch && sat)) b.pt[7] += 1ull << 16;
+    if (ballot(((Mv >> lane) & 1ull) && (eq & ins & ((1ull << lane) - 1ull)))) b.pt[7] += 1ull << 32;
+    if (mode == W_SEARCH && b.cnt + x1 > 64) b.pt[7] += 1ull << 48;
+#endif
     if (!ballot(bad) && !(mode == W_SEARCH && b.cnt + x1 > 64)) {
       fast_done = true;
       seq_prev = prev;
@@ -783,6 +789,10 @@ __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table,
            (unsigned long long)b.pn, (unsigned long long)(__builtin_amdgcn_s_memtime() - tstart_), (unsigned long long)b.pt[0],
            (unsigned long long)b.pt[1], (unsigned long long)b.pt[2], (unsigned long long)b.pt[3], (unsigned long long)b.pt[4],
            (unsigned long long)b.pt[5], (unsigned long long)b.pt[6]);
+  if (lane == 0 && (blockIdx.x % 509) == 0)
+    printf("WINWHY blk %u longback %llu sat %llu inwin %llu stride %llu\n", blockIdx.x, (unsigned long long)(b.pt[7] & 0xFFFF),
+           (unsigned long long)((b.pt[7] >> 16) & 0xFFFF), (unsigned long long)((b.pt[7] >> 32) & 0xFFFF),
+           (unsigned long long)(b.pt[7] >> 48));
 #endif
   // last literals (lz4.c:1141-1166)
   const uint32_t last = uint32_t(n - b.anchor);

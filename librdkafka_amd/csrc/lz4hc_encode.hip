@@ -554,18 +554,21 @@ __device__ __forceinline__ bool hc_sure_miss(const HcBlock &b, int p, int mflimi
   const int r = int(t >> 16);
   const int total = r < b.attempts ? r : b.attempts;
   const int top = int(t & 0xFFFFu) - 1;
+  // positions that cannot be settled here read nothing of their own (their loads go to the
+  // position itself, a line the wave has already touched)
+  const bool open = !in || rep || total > 8;
+  const int nt = open ? 0 : total;
   int c[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) c[j] = int(b.sorted[j < total ? top - j : 0]);
+  for (int j = 0; j < 8; ++j) c[j] = int(b.sorted[j < nt ? top - j : 0]);
   uint32_t w[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) w[j] = ld32u_nb(b.s + (j < total ? c[j] : pc));
+  for (int j = 0; j < 8; ++j) w[j] = ld32u_nb(b.s + (j < nt ? c[j] : pc));
   bool miss = true;
 #pragma unroll
   for (int j = 0; j < 8; ++j)
-    if (j < total && w[j] == pat) miss = false;
-  if (!in || rep || total > 8) return false;
-  return miss;  // (total == 0: nothing to test)
+    if (j < nt && w[j] == pat) miss = false;
+  return !open && miss;  // (total == 0: nothing to test)
 }
 
 // LZ4HC_compress_hashChain (lz4hc.c:532-746).  Returns the compressed size or

@@ -495,45 +495,82 @@ __device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int long
   return longest;
 }
 
-// LZ4HC_encodeSequence (lz4hc.c:462-530), limitedOutput: 0 ok, 1 overflow
-__device__ int hc_encode(const HcBlock &b, uintptr_t d, int &op, int oend, int &ip, int &anchor,
-                         int ml, int ref) {
+// Sequences are queued, one per lane (literal start | literal length << 16, offset |
+// matchlength-4 << 16), and written out 64 at a time: one round trip fetches the literals of
+// 64 sequences, where writing each sequence as it is found costs one per sequence.
+struct HcQueue {
+  uint32_t q0, q1;
+  int qn;
+  int n;  // block size (bounds of the literal windows and the output stores)
+};
+
+// LZ4HC_encodeSequence (lz4hc.c:462-530), limitedOutput, for the queued sequences: 0 ok,
+// 1 overflow (the block is stored raw, whichever sequence overflowed)
+__device__ int hc_flush(const HcBlock &b, uintptr_t d, int &op, int oend, HcQueue &q) {
   const int lane = b.lane;
-  int o = op;
-  const int tok = o++;
-  const int lit = ip - anchor;
-  if (o + lit / 255 + lit + (2 + 1 + kLz4LastLiterals) > oend) return 1;
-  uint32_t token;
-  if (lit >= 15) {
-    const int l = lit - 15;
-    token = 15u << 4;
-    hc_run(d + o, l / 255, l % 255, lane);
-    o += l / 255 + 1;
-  } else {
-    token = uint32_t(lit) << 4;
+  const bool ch = lane < q.qn;
+  const uint32_t lstart = q.q0 & 0xFFFFu, lit = ch ? q.q0 >> 16 : 0u;
+  const uint32_t off = q.q1 & 0xFFFFu, l = q.q1 >> 16;
+  const uint32_t lext = ext_bytes(lit);
+  const uint32_t sz = ch ? 3u + lit + lext + ext_bytes(l) : 0u;
+  uint32_t tot;
+  const uint32_t tp = uint32_t(op) + wave_excl_scan(sz, tot);  // token
+  const uint32_t lp = tp + 1u + lext;                          // first literal
+  const uint32_t fp = lp + lit;                                // offset field
+  const bool ov = ch && (int(tp + 1u + lit / 255u + lit + (2u + 1u + kLz4LastLiterals)) > oend ||
+                         int(fp + 2u + l / 255u + (1u + kLz4LastLiterals)) > oend);
+  if (ballot(ov)) return 1;
+  const uintptr_t lo = b.s & ~uintptr_t(3);
+  const rsrc_t rs = block_rsrc(lo, (b.s + uint32_t(q.n) + 3u) & ~uintptr_t(3));
+  const uint32_t sa = uint32_t(b.s & 3u);
+  const rsrc_t wd = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(d), 0, q.n, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b8(
+      uint8_t(((lit < 15u ? lit : 15u) << 4) | (l < 15u ? l : 15u)), wd, ch ? tp : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off), wd, ch ? fp : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(off >> 8), wd, ch ? fp + 1u : kNoLoad, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(l - 15u), wd,
+                                       (ch && l >= 15u && l < 270u) ? fp + 2u : kNoLoad, 0, 0);
+  if (ballot(ch && lit >= 15u)) {
+    if (ch && lit >= 15u) put_len(d + tp + 1u, lit);
   }
-  hc_copy(d + o, b.s + anchor, lit, lane);
-  o += lit;
-  const int off = ip - ref;
-  if (lane == 0) {
-    stb(d + o, uint32_t(off) & 0xFFu);
-    stb(d + o + 1, (uint32_t(off) >> 8) & 0xFFu);
+  if (ballot(ch && l >= 270u)) {
+    if (ch && l >= 270u) put_len(d + fp + 2u, l);
   }
-  o += 2;
-  int l = ml - kLz4MinMatch;
-  if (o + l / 255 + (1 + kLz4LastLiterals) > oend) return 1;
-  if (l >= 15) {
-    token += 15u;
-    l -= 15;
-    hc_run(d + o, l / 255, l % 255, lane);
-    o += l / 255 + 1;
-  } else {
-    token += uint32_t(l);
+  const bool need_win = ch && lit != 0u && lit <= 16u;
+  if (ballot(need_win)) {  // up to 16 literals: one 20-byte window per lane
+    uint32_t w[5];
+    load5(rs, need_win ? ((lstart + sa) & ~3u) : kNoLoad, w);
+    const uint32_t sh = (lstart + sa) & 3u;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+#pragma unroll
+    for (uint32_t k = 0; k < 16u; ++k)
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[k >> 2] >> (8u * (k & 3u))), wd,
+                                           (need_win && k < lit) ? lp + k : kNoLoad, 0, 0);
   }
-  if (lane == 0) stb(d + tok, token);
+  uint64_t longm = ballot(ch && lit > 16u);  // long runs: the whole wave copies them
+  while (longm) {
+    const int j = __builtin_ctzll(longm);
+    longm &= longm - 1;
+    hc_copy(d + __builtin_amdgcn_readlane(lp, j), b.s + __builtin_amdgcn_readlane(lstart, j),
+            int(__builtin_amdgcn_readlane(lit, j)), lane);
+  }
+  op += int(tot);
+  q.qn = 0;
+  return 0;
+}
+
+// queue the sequence (literals anchor..ip, match of ml bytes at ref) and step over it
+__device__ __forceinline__ int hc_encode(const HcBlock &b, uintptr_t d, int &op, int oend, int &ip,
+                                         int &anchor, int ml, int ref, HcQueue &q) {
+  if (q.qn == 64 && hc_flush(b, d, op, oend, q)) return 1;
+  const bool me = b.lane == q.qn;
+  q.q0 = me ? uint32_t(anchor) | (uint32_t(ip - anchor) << 16) : q.q0;
+  q.q1 = me ? uint32_t(ip - ref) | (uint32_t(ml - kLz4MinMatch) << 16) : q.q1;
+  q.qn++;
   ip += ml;
   anchor = ip;
-  op = o;
   return 0;
 }
 
@@ -584,6 +621,7 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool pr
   int nskip = 0;
 #endif
   int ip = 0, anchor = 0, op = 0, unused = 0;
+  HcQueue q = {0u, 0u, 0, n};
   int ml, ml0, ml2, ml3, start0, ref0, ref = 0, start2 = 0, ref2 = 0, start3 = 0, ref3 = 0;
   int wbase = 0, wend = 0;  // positions [wbase, wend) have a sure-miss bit in wmiss
   uint64_t wmiss = 0;
@@ -610,7 +648,7 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool pr
     else
       ml2 = ml;
     if (ml2 == ml) {
-      if (hc_encode(b, dst, op, oend, ip, anchor, ml, ref)) return 0;
+      if (hc_encode(b, dst, op, oend, ip, anchor, ml, ref, q)) return 0;
       continue;
     }
     if (start0 < ip && start2 < ip + ml0) { ip = start0; ref = ref0; ml = ml0; }
@@ -628,9 +666,9 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool pr
       ml3 = ml2;
     if (ml3 == ml2) {
       if (start2 < ip + ml) ml = start2 - ip;
-      if (hc_encode(b, dst, op, oend, ip, anchor, ml, ref)) return 0;
+      if (hc_encode(b, dst, op, oend, ip, anchor, ml, ref, q)) return 0;
       ip = start2;
-      if (hc_encode(b, dst, op, oend, ip, anchor, ml2, ref2)) return 0;
+      if (hc_encode(b, dst, op, oend, ip, anchor, ml2, ref2, q)) return 0;
       continue;
     }
     if (start3 < ip + ml + 3) {
@@ -640,7 +678,7 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool pr
           start2 += corr; ref2 += corr; ml2 -= corr;
           if (ml2 < kLz4MinMatch) { start2 = start3; ref2 = ref3; ml2 = ml3; }
         }
-        if (hc_encode(b, dst, op, oend, ip, anchor, ml, ref)) return 0;
+        if (hc_encode(b, dst, op, oend, ip, anchor, ml, ref, q)) return 0;
         ip = start3; ref = ref3; ml = ml3;
         start0 = start2; ref0 = ref2; ml0 = ml2;
         goto search2;
@@ -658,11 +696,12 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool pr
         ml = start2 - ip;
       }
     }
-    if (hc_encode(b, dst, op, oend, ip, anchor, ml, ref)) return 0;
+    if (hc_encode(b, dst, op, oend, ip, anchor, ml, ref, q)) return 0;
     ip = start2; ref = ref2; ml = ml2;
     start2 = start3; ref2 = ref3; ml2 = ml3;
     goto search3;
   }
+  if (hc_flush(b, dst, op, oend, q)) return 0;
   {  // last literals (lz4hc.c:709-734)
     const int run = n - anchor;
     if (op + 1 + (run + 255 - 15) / 255 + run > oend) return 0;
@@ -822,13 +861,14 @@ __device__ int hc_optimal_block(const HcBlock &b, uintptr_t dst, int n, int suff
   if (!prebuilt) hc_build(b, mflimit + 1);
   if (sufficient >= kHcOptNum) sufficient = kHcOptNum - 1;
   int ip = 0, anchor = 0, op = 0;
+  HcQueue q = {0u, 0u, 0, n};
   while (ip <= mflimit) {
     const int llen = ip - anchor;
     int best_mlen, best_off, cur, last_pos, foff = 0;
     const int flen = hc_longer(b, ip, matchlimit, kLz4MinMatch - 1, foff);
     if (flen == 0) { ip++; continue; }
     if (flen > sufficient) {  // good enough: immediate encoding (lz4hc.c:1318-1326)
-      if (hc_encode(b, dst, op, oend, ip, anchor, flen, ip - foff)) return 0;
+      if (hc_encode(b, dst, op, oend, ip, anchor, flen, ip - foff, q)) return 0;
       continue;
     }
     // prices of the first positions: literals (lz4hc.c:1329-1338), then the first match at
@@ -921,10 +961,11 @@ __device__ int hc_optimal_block(const HcBlock &b, uintptr_t dst, int n, int suff
         if (ml == 1) { ip++; r++; continue; }
         const int off = int(__builtin_amdgcn_readlane(e.y, r - rb));
         r += ml;
-        if (hc_encode(b, dst, op, oend, ip, anchor, ml, ip - off)) return 0;
+        if (hc_encode(b, dst, op, oend, ip, anchor, ml, ip - off, q)) return 0;
       }
     }
   }
+  if (hc_flush(b, dst, op, oend, q)) return 0;
   {  // last literals (lz4hc.c:1501-1526)
     const int run = n - anchor;
     if (op + 1 + (run + 255 - 15) / 255 + run > oend) return 0;

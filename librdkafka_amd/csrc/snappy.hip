@@ -891,10 +891,16 @@ struct SnCand {
   uint32_t A, ll, off, mk;  // mk = ml | k << 8
 };
 
-__device__ __forceinline__ SnCand sn_parse(const SnDec &d, uint32_t csize, uint32_t seg, int lane) {
-  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+typedef uint32_t sn_u2 __attribute__((ext_vector_type(2)));
+
+// the aligned 8 bytes that hold the 4 bytes at p = seg + lane
+__device__ __forceinline__ sn_u2 sn_parse_load(const SnDec &d, uint32_t seg, int lane) {
+  return __builtin_amdgcn_raw_buffer_load_b64(d.rin, (seg + uint32_t(lane) + d.din) & ~3u, 0, 0);
+}
+
+__device__ __forceinline__ SnCand sn_parse_words(const SnDec &d, sn_u2 h, uint32_t csize, uint32_t seg,
+                                                 int lane) {
   const uint32_t p = seg + uint32_t(lane);
-  const u2 h = __builtin_amdgcn_raw_buffer_load_b64(d.rin, (p + d.din) & ~3u, 0, 0);
   const uint32_t w = __builtin_amdgcn_alignbyte(h.y, h.x, (p + d.din) & 3u);
   const uint32_t c = w & 0xFFu, kind = c & 3u, hi = c >> 2;
   const uint32_t b1 = (w >> 8) & 0xFFu, b12 = (w >> 8) & 0xFFFFu, b123 = w >> 8;
@@ -915,40 +921,26 @@ __device__ __forceinline__ SnCand sn_parse(const SnDec &d, uint32_t csize, uint3
   return r;
 }
 
+__device__ __forceinline__ SnCand sn_parse(const SnDec &d, uint32_t csize, uint32_t seg, int lane) {
+  return sn_parse_words(d, sn_parse_load(d, seg, lane), csize, seg, lane);
+}
+
 // wave-uniform byte of the stream (slow path only)
 __device__ __forceinline__ uint32_t sn_in_byte(const SnDec &d, uint32_t i) {
   return __builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b8(d.rin, i + d.din, 0, 0));
 }
 
-// Decode the stream at `src` (n bytes) into `dst` (cap bytes).  Returns 0 or -EIO like
-// rd_kafka_snappy_uncompress; *ulen_out = the declared length (0 when unreadable).
 #ifdef RDK_SN_DEBUG
 #define SN_FAIL(site) (kSnEIO - 100 * (site))
 #else
 #define SN_FAIL(site) kSnEIO
 #endif
-__device__ int sn_decode_stream(uintptr_t src, uint32_t n, uintptr_t dst, uint32_t cap,
-                                uint32_t *ulen_out, sn_lds_u8 *ring, sn_lds_u8 *map, int lane) {
-  if (n >= 0x80000000u) return SN_FAIL(1);  // input positions carry a tag in bit 31
-  SnDec d;
-  d.ring = ring;
-  d.map = map;
-  d.din = uint32_t(src & 3u);
-  d.rin = sn_make_rsrc(src - d.din, (d.din + n + 3u) & ~3u);
-  d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
-  // read_uncompressed_length (snappy.c:1193-1218)
-  uint32_t ulen = 0, ip0 = 0;
-  for (uint32_t shift = 0;; shift += 7u) {
-    if (shift >= 32u || ip0 >= n) return SN_FAIL(2);
-    const uint32_t c = sn_in_byte(d, ip0++);
-    ulen |= (c & 0x7Fu) << shift;
-    if (c < 128u) break;
-  }
-  *ulen_out = ulen;
-  if (ulen > 0x7FFFFFF0u) return SN_FAIL(3);  // positions are kept in 31 bits
-  if (ulen > cap) return kSnDstSize;      // the caller sizes dst from the preamble
-  d.rout = sn_make_rsrc(dst, ulen);
-  uint32_t op = 0, ipn = ip0;
+// The elements of the stream from input position ipn up to n, which must produce exactly
+// `ulen` bytes from output position 0 of d.rout (decompress_all_tags, snappy.c:1226-1312).
+// Returns 0 or -EIO.
+__device__ int sn_decode_elems(SnDec &d, uint32_t n, uint32_t ipn, uint32_t ulen, sn_lds_u8 *map,
+                               int lane) {
+  uint32_t op = 0;
   if (ipn == n) return ulen == 0u ? 0 : SN_FAIL(21);
   uint32_t seg = ipn & ~63u;
   SnCand cur = sn_parse(d, n, seg, lane);
@@ -1052,11 +1044,161 @@ __device__ int sn_decode_stream(uintptr_t src, uint32_t n, uintptr_t dst, uint32
   }
 }
 
+// Decode the stream at `src` (n bytes) into `dst` (cap bytes).  Returns 0 or -EIO like
+// rd_kafka_snappy_uncompress; *ulen_out = the declared length (0 when unreadable).
+__device__ int sn_decode_stream(uintptr_t src, uint32_t n, uintptr_t dst, uint32_t cap,
+                                uint32_t *ulen_out, sn_lds_u8 *ring, sn_lds_u8 *map, int lane) {
+  if (n >= 0x80000000u) return SN_FAIL(1);  // input positions carry a tag in bit 31
+  SnDec d;
+  d.ring = ring;
+  d.map = map;
+  d.din = uint32_t(src & 3u);
+  d.rin = sn_make_rsrc(src - d.din, (d.din + n + 3u) & ~3u);
+  d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
+  // read_uncompressed_length (snappy.c:1193-1218)
+  uint32_t ulen = 0, ip0 = 0;
+  for (uint32_t shift = 0;; shift += 7u) {
+    if (shift >= 32u || ip0 >= n) return SN_FAIL(2);
+    const uint32_t c = sn_in_byte(d, ip0++);
+    ulen |= (c & 0x7Fu) << shift;
+    if (c < 128u) break;
+  }
+  *ulen_out = ulen;
+  if (ulen > 0x7FFFFFF0u) return SN_FAIL(3);  // positions are kept in 31 bits
+  if (ulen > cap) return kSnDstSize;      // the caller sizes dst from the preamble
+  d.rout = sn_make_rsrc(dst, ulen);
+  return sn_decode_elems(d, n, ip0, ulen, map, lane);
+}
+
+// ---- decoding a stream by its fragments
+// A compressor emits one run of elements per 64 KiB fragment of its input (sn_compress,
+// snappy.c:1408-1484), so in the streams it makes no element crosses a multiple of 64 KiB of
+// output and no copy reaches in front of its fragment.  A parse-only pass over the stream
+// (one wave per stream, nothing written) checks exactly that and notes where in the input
+// each fragment starts; the fragments are then decoded independently, which fills the chip
+// where one wave per stream leaves it nearly idle.  A stream that is anything else --
+// malformed, a single fragment, elements or copies that cross -- is decoded serially as
+// before, and that decoder alone decides its verdict.
+constexpr uint32_t kSnFragMax = 64;  // fragments per stream the split handles (4 MiB)
+
+struct SnSplit {
+  int32_t split;            // 1: decode by fragments; 0: decode the stream serially
+  uint32_t ulen, ip0, nfrag;
+  uint32_t ip[kSnFragMax];  // input position of fragment k's first element (k >= 1)
+};
+
+__device__ bool sn_scan_stream(uintptr_t src, uint32_t n, uint32_t cap, SnSplit *t, int lane) {
+  if (n >= 0x80000000u) return false;
+  SnDec d;
+  d.ring = nullptr;
+  d.map = nullptr;
+  d.din = uint32_t(src & 3u);
+  d.rin = sn_make_rsrc(src - d.din, (d.din + n + 3u) & ~3u);
+  d.rout = d.rin;
+  d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
+  uint32_t ulen = 0, ip0 = 0;
+  for (uint32_t shift = 0;; shift += 7u) {
+    if (shift >= 32u || ip0 >= n) return false;
+    const uint32_t c = sn_in_byte(d, ip0++);
+    ulen |= (c & 0x7Fu) << shift;
+    if (c < 128u) break;
+  }
+  const uint32_t nfrag = (ulen + kSnBlock - 1u) / kSnBlock;
+  if (ulen > cap || nfrag < 2u || nfrag > kSnFragMax || ip0 == n) return false;
+  uint32_t op = 0, ipn = ip0, found = 0;
+  uint32_t seg = ipn & ~63u;
+  SnCand cur = sn_parse(d, n, seg, lane);
+  // this pass runs at one wave per SIMD with nothing to hide a load behind: the header
+  // bytes of the next four segments are in flight
+  sn_u2 pf[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pf[j] = sn_parse_load(d, seg + 64u * uint32_t(j + 1), lane);
+  for (;;) {
+    const uint32_t x0 = ipn - seg;
+    const bool stop = (cur.A - seg >= 64u) | (cur.A == n);
+    uint32_t J = stop ? 64u : cur.A - seg;
+    bool R = uint32_t(lane) == x0;
+#pragma unroll
+    for (int level = 0; level < 5; ++level) {
+      const bool send = R & (J < 64u);
+      const int tt = __builtin_amdgcn_ds_permute(int((send ? J : x0) << 2), int(send));
+      R = R | (tt != 0);
+      const uint32_t jj = uint32_t(__shfl(int(J), int(J & 63u)));
+      J = J < 64u ? jj : 64u;
+    }
+    const uint64_t M = sn_ballot(R);
+    if (sn_ballot(R & ((cur.A == kSnBad) | (cur.A == kSnComplex)))) return false;
+    const uint32_t xl = uint32_t(63 - __builtin_clzll(M));
+    const uint32_t a_last = uni(__builtin_amdgcn_readlane(cur.A, xl));
+    if (a_last > n) return false;
+    const bool mem = (M >> lane) & 1ull;
+    const uint32_t ll = cur.ll, ml = cur.mk & 0xFFu, off = cur.off;
+    const uint32_t len = mem ? ll + ml : 0u;
+    uint32_t T;
+    const uint32_t ostart = op + sn_excl_sum(len, T);
+    if (uint64_t(op) + T > ulen) return false;
+    const uint32_t in_frag = ostart & (kSnBlock - 1u);
+    const bool crosses = mem & (in_frag + len > kSnBlock);
+    const bool reaches = mem & (ml != 0u) & (in_frag <= off - 1u);  // offset 0, or in front of the fragment
+    if (sn_ballot(crosses | reaches)) return false;
+    const bool first = mem & (in_frag == 0u) & (ostart != 0u);
+    if (first) t->ip[ostart >> 16] = seg + uint32_t(lane);
+    found += uint32_t(__builtin_popcountll(sn_ballot(first)));
+    op = uni(op + T);
+    if (a_last == n) break;
+    ipn = a_last;
+    const uint32_t nseg = ipn & ~63u;
+    if (nseg == seg + 64u) {
+      cur = sn_parse_words(d, pf[0], n, nseg, lane);
+      pf[0] = pf[1];
+      pf[1] = pf[2];
+      pf[2] = pf[3];
+      pf[3] = sn_parse_load(d, nseg + 256u, lane);
+    } else {  // a literal ran over whole segments
+      cur = sn_parse(d, n, nseg, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pf[j] = sn_parse_load(d, nseg + 64u * uint32_t(j + 1), lane);
+    }
+    seg = nseg;
+  }
+  if (op != ulen || found != nfrag - 1u) return false;
+  if (lane == 0) {
+    t->ulen = ulen;
+    t->ip0 = ip0;
+    t->nfrag = nfrag;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(64 * kSnDecWaves) void snappy_scan_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
+    const uint32_t *__restrict__ in_lens, const uint32_t *__restrict__ out_caps,
+    uint32_t *__restrict__ out_lens, int32_t *__restrict__ status, SnSplit *__restrict__ tab,
+    uint32_t n) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t w = uni(threadIdx.x >> 6);
+  const uint32_t wpb = blockDim.x >> 6;
+  for (uint32_t f = blockIdx.x * wpb + w; f < n; f += gridDim.x * wpb) {
+    const uintptr_t src = reinterpret_cast<uintptr_t>(in) + in_offs[f];
+    SnSplit *t = tab + f;
+    const bool ok = sn_scan_stream(src, uni(in_lens[f]), uni(out_caps[f]), t, lane);
+    if (lane == 0) {
+      t->split = ok ? 1 : 0;
+      if (ok) {  // the fragments only report failures
+        status[f] = 0;
+        out_lens[f] = t->ulen;
+      }
+    }
+  }
+}
+
+// items (fragment slot k, stream f), slot-major: fragment k of a split stream, or (k == 0) a
+// whole stream that is decoded serially
 __global__ __launch_bounds__(64 * kSnDecWaves) void snappy_uncompress_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
     const uint32_t *__restrict__ out_caps, uint32_t *__restrict__ out_lens,
-    int32_t *__restrict__ status, uint32_t n) {
+    int32_t *__restrict__ status, const SnSplit *__restrict__ tab, uint32_t n) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kSnDecWaves][kSnRing];
   __shared__ __attribute__((aligned(16))) uint8_t maps[kSnDecWaves][128];
   const int lane = threadIdx.x & 63;
@@ -1064,14 +1206,35 @@ __global__ __launch_bounds__(64 * kSnDecWaves) void snappy_uncompress_kernel(
   sn_lds_u8 *ring = (sn_lds_u8 *)rings[w];
   sn_lds_u8 *map = (sn_lds_u8 *)maps[w];
   const uint32_t wpb = blockDim.x >> 6;
-  for (uint32_t f = blockIdx.x * wpb + w; f < n; f += gridDim.x * wpb) {
+  const uint64_t items = uint64_t(n) * kSnFragMax;
+  for (uint64_t it = uint64_t(blockIdx.x) * wpb + w; it < items; it += uint64_t(gridDim.x) * wpb) {
+    const uint32_t f = uint32_t(it % n), k = uint32_t(it / n);
+    const SnSplit *t = tab + f;
     const uintptr_t src = reinterpret_cast<uintptr_t>(in) + in_offs[f];
     const uintptr_t dst = reinterpret_cast<uintptr_t>(out) + out_offs[f];
-    uint32_t ulen = 0;
-    const int r = sn_decode_stream(src, uni(in_lens[f]), dst, uni(out_caps[f]), &ulen, ring, map, lane);
-    if (lane == 0) {
-      status[f] = r;
-      out_lens[f] = ulen;
+    if (uni(uint32_t(t->split))) {
+      const uint32_t nfrag = uni(t->nfrag);
+      if (k >= nfrag) continue;
+      const uint32_t nin = uni(in_lens[f]), ulen = uni(t->ulen);
+      const uint32_t ipk = k ? uni(t->ip[k]) : uni(t->ip0);
+      const uint32_t ipe = k + 1u < nfrag ? uni(t->ip[k + 1u]) : nin;
+      const uint32_t flen = k + 1u < nfrag ? kSnBlock : ulen - k * kSnBlock;
+      SnDec d;
+      d.ring = ring;
+      d.map = map;
+      d.din = uint32_t(src & 3u);
+      d.rin = sn_make_rsrc(src - d.din, (d.din + nin + 3u) & ~3u);
+      d.rout = sn_make_rsrc(dst + uint64_t(k) * kSnBlock, flen);
+      d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
+      const int r = sn_decode_elems(d, ipe, ipk, flen, map, lane);
+      if (r != 0 && lane == 0) status[f] = r;
+    } else if (k == 0) {
+      uint32_t ulen = 0;
+      const int r = sn_decode_stream(src, uni(in_lens[f]), dst, uni(out_caps[f]), &ulen, ring, map, lane);
+      if (lane == 0) {
+        status[f] = r;
+        out_lens[f] = ulen;
+      }
     }
   }
 }
@@ -1104,12 +1267,21 @@ int snappy_uncompress_device(const uint8_t *d_in, const uint64_t *d_in_offs, con
                              uint8_t *d_out, const uint64_t *d_out_offs, const uint32_t *d_out_caps,
                              uint32_t *d_out_lens, int32_t *d_status, uint32_t n, hipStream_t s) {
   if (!n) return 0;
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  // the per-stream fragment tables live in the decoder's scratch region (stream-ordered)
+  int rc = scratch_acquire(c, kScratchDecode, size_t(n) * sizeof(SnSplit), s);
+  if (rc) return rc;
+  SnSplit *tab = reinterpret_cast<SnSplit *>(c->d_stage[kScratchDecode]);
   const unsigned wg = (n + kSnDecWaves - 1) / kSnDecWaves;
-  hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(wg < 2048u ? wg : 2048u), dim3(64 * kSnDecWaves), 0,
-                     s, d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_caps, d_out_lens, d_status,
-                     n);
+  hipLaunchKernelGGL(snappy_scan_kernel, dim3(wg < 2048u ? wg : 2048u), dim3(64 * kSnDecWaves), 0, s,
+                     d_in, d_in_offs, d_in_lens, d_out_caps, d_out_lens, d_status, tab, n);
+  const uint64_t wgi = (uint64_t(n) * kSnFragMax + kSnDecWaves - 1) / kSnDecWaves;
+  hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(unsigned(wgi < 2048u ? wgi : 2048u)),
+                     dim3(64 * kSnDecWaves), 0, s, d_in, d_in_offs, d_in_lens, d_out, d_out_offs,
+                     d_out_caps, d_out_lens, d_status, tab, n);
   RDK_HIP_CHECK(hipGetLastError());
-  return 0;
+  return scratch_release(c, kScratchDecode, s);
 }
 
 }  // namespace rdk

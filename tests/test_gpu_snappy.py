@@ -117,6 +117,44 @@ def test_batch_uncompress_own_and_foreign_streams(engine, oracle_mod):
             assert st == 0 and out == d, (i, st, len(d), len(out))
 
 
+def test_uncompress_streams_that_do_not_split(engine, oracle_mod):
+    """valid streams no compressor of 64 KiB fragments would make: a copy that reaches into the
+    previous 64 KiB of output, an element that crosses a multiple of 64 KiB, more than 64
+    fragments -- the parse-only pass must hand them to the serial decoder -- next to split ones"""
+    pa = pytest.importorskip("pyarrow")
+    rnd = random.Random(31)
+
+    def varint(n):
+        out = bytearray()
+        while n >= 128:
+            out.append((n & 127) | 128)
+            n >>= 7
+        out.append(n)
+        return bytes(out)
+
+    def literal(b):
+        n = len(b) - 1
+        if n < 60:
+            return bytes([n << 2]) + b
+        k = (n.bit_length() + 7) // 8
+        return bytes([(59 + k) << 2]) + n.to_bytes(k, "little") + b
+
+    a = rnd.randbytes(65536)
+    b = W.gen_json(70000, 5)
+    reach = varint(65536 + 8) + literal(a) + bytes([2 | (7 << 2), 100, 0])          # copy2 len 8 off 100
+    cross = varint(70000) + literal(b)                                               # one literal over the boundary
+    cross2 = varint(65536 + 40) + literal(a[:65530]) + bytes([2 | (45 << 2), 9, 0])  # copy over the boundary
+    big = oracle_mod.snappy_compress(W.gen_json(65 * 65536 + 5, 6))                  # 66 fragments
+    ok = oracle_mod.snappy_compress(W.gen_json(5 * 65536 + 77, 7))                   # splits
+    streams = [reach, cross, cross2, big, ok]
+    want = [oracle_mod.snappy_uncompress(x) for x in streams]
+    assert all(w[0] == 0 for w in want)
+    assert want[0][1] == a + a[65436:65444] and want[1][1] == b
+    for x, w in zip(streams[:3], want[:3]):
+        assert pa.decompress(x, decompressed_size=len(w[1]), codec="snappy", asbytes=True) == w[1]
+    assert _uncompress_batch(engine, streams) == want
+
+
 def test_uncompress_verdicts_on_damaged_streams(engine, oracle_mod):
     rnd = random.Random(9)
     base = [W.gen_json(5000, 4), bytes(3000) + W.gen_json(2000, 1), (rnd.randbytes(100) * 60)]

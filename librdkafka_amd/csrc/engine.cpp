@@ -273,5 +273,5 @@ RDK_API int rdk_hip_init(int device) {
 RDK_API const char *rdk_hip_last_error(void) { return rdk::last_error(); }
 
 RDK_API const char *rdk_hip_version(void) {
-  return "librdkafka_hip 0.3 gfx950 crc32c:group16-bytetab-lds lz4c:window64-exact+round64-fast+fused-crc lz4hc:3-9 lz4d:seg64-parallel";
+  return "librdkafka_hip 0.4 gfx950 crc32c:group16-bytetab-lds lz4c:window64-exact+round64-fast+fused-crc+seq-queue lz4hc:3-12-lds-build lz4d:seg64-parallel snappy:window64-exact+fragment-decode";
 }

@@ -96,13 +96,15 @@ def test_hc_levels_above_12_clamp(engine, oracle_mod):
 
 
 def test_batch_hc_many_frames_queue_and_scratch_growth(engine, oracle_mod):
-    """96 x 1 MiB at level 9 after a one-frame call: 1536 block items over a grid that was
-    last sized for 16 (the scratch grows), and at the full 4096-wave grid every wave takes
-    its blocks from the work queue.  Four distinct inputs rotate, so the oracle runs 4x."""
+    """96 and 272 x 1 MiB at level 9 after a one-frame call: 1536 block items over a scratch that
+    was last sized for 16 (it grows), then 4352 blocks in two chunks of the build and parse
+    kernels.  Four distinct inputs rotate, so the oracle runs 4x."""
     import torch
     distinct = [W.gen_json(1 << 20, 90 + i) for i in range(4)]
     want = [oracle_mod.rdk_lz4_compress(b, comp_level=9)[1] for b in distinct]
-    for inputs in ([distinct[0]], [distinct[i % 4] for i in range(96)]):
+    # 272 frames: 4352 blocks, more than one 4096-item chunk of the build / parse kernels holds
+    for inputs in ([distinct[0]], [distinct[i % 4] for i in range(96)],
+                   [distinct[i % 4] for i in range(272)]):
         hbuf, hoffs = _pack(inputs)
         d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
         in_offs = torch.tensor(hoffs, dtype=torch.int64, device="cuda")

@@ -76,7 +76,20 @@ struct HcBlock {
   int attempts;      // nbSearches
   int pa;            // patternAnalysis (levels 9+)
   int lane;
+#ifdef RDK_HC_PROF
+  mutable uint64_t pc[10];
+#endif
 };
+
+#ifdef RDK_HC_PROF
+#define HC_T0() const uint64_t hct0_ = __builtin_amdgcn_s_memtime()
+#define HC_ADD(k) b.pc[k] += __builtin_amdgcn_s_memtime() - hct0_
+#define HC_CNT(k, v) b.pc[k] += (v)
+#else
+#define HC_T0() do { } while (0)
+#define HC_ADD(k) do { } while (0)
+#define HC_CNT(k, v) do { } while (0)
+#endif
 
 __device__ __forceinline__ uint32_t hc_hash(uint32_t v) {  // HASH_FUNCTION, lz4hc.c:81
   return (v * 2654435761u) >> (32 - kHcHashLog);
@@ -420,8 +433,18 @@ __device__ __forceinline__ void hc_load_words(uintptr_t a, uint32_t w[N]) {
 // candidate's 36 bytes (the MINMATCH test and the first 32 bytes of LZ4_count) and the 8
 // bytes in front of it (countBack), on clamped addresses; the source's windows are loaded
 // once, with the pattern and the table entry.  Longer matches continue from memory.
+__device__ int hc_search_w(const HcBlock &b, int ip, int ilow, int ihigh, int longest, int &mpos,
+                           int &spos);
 __device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int longest, int &mpos,
                          int &spos) {
+  HC_T0();
+  const int r_ = hc_search_w(b, ip, ilow, ihigh, longest, mpos, spos);
+  HC_ADD(ip == ilow ? 0 : 1);
+  HC_CNT(ip == ilow ? 2 : 3, 1);
+  return r_;
+}
+__device__ int hc_search_w(const HcBlock &b, int ip, int ilow, int ihigh, int longest, int &mpos,
+                           int &spos) {
   if (ip + 48 > ihigh) return hc_search_edge(b, ip, ilow, ihigh, longest, mpos, spos);
   const uintptr_t s = b.s;
   const int lane = b.lane;
@@ -433,11 +456,15 @@ __device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int long
   hc_load_words<2>(s + (wideback ? ip - 8 : ip), sb);  // bytes ip-8 .. ip
   const uint32_t pat = sw[0];
   if (b.pa && ((pat & 0xFFFFu) == (pat >> 16)) && ((pat & 0xFFu) == (pat >> 24)))
+  {
+    HC_CNT(5, 1);
     return hc_search_serial(b, ip, ilow, ihigh, longest, mpos, spos, pat, false);
+  }
   const int r = int(t >> 16);
   const int top = int(t & 0xFFFFu) - 1;  // sorted[top] = latest earlier same-hash
   const int total = r < b.attempts ? r : b.attempts;
   for (int c0 = 0; c0 < total; c0 += 64) {
+    HC_CNT(4, 1);
     const int j = c0 + lane;
     const bool valid = j < total;
     const int c = int(b.sorted[valid ? top - j : top]);
@@ -469,11 +496,14 @@ __device__ int hc_search(const HcBlock &b, int ip, int ilow, int ihigh, int long
     const int len = ok32 ? 4 + fwd - back : 0;
     int k0 = 0;
     for (;;) {  // the reference's order: first improving candidate at the current longest
-      // the read16 prefilter at longest-1 from the low limit (lz4hc.c:264): both of its bytes
-      // lie inside the measured match when that reaches back to the low limit (always, for
-      // a search without look-back), so only the other candidates have to read them
+      // the read16 prefilter (lz4hc.c:264) compares the bytes at offsets o and o+1 from ip,
+      // o = longest-1 - look-back.  The measured match covers offsets [back, back+len): o+1
+      // lies below its end for a candidate that beats `longest` (len > longest, back >= -br),
+      // and o lies in it unless the backward count stopped above o -- never for the searches
+      // of the hash-chain parser (o is 2, 1 and 2 for its three searches and only grows), so
+      // nothing is read for the prefilter
       const bool cand = ok32 && lane >= k0 && len > longest;
-      const bool sure = back == -br;
+      const bool sure = longest - 1 - br >= back;
       bool pass = cand && sure;
       if (ballot(cand && !sure)) {
         const bool rd = cand && !sure;
@@ -619,6 +649,7 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool pr
 #ifdef RDK_HC_PROF
   const uint64_t t1 = wall_clock64();
   int nskip = 0;
+  for (int k = 0; k < 10; ++k) b.pc[k] = 0;
 #endif
   int ip = 0, anchor = 0, op = 0, unused = 0;
   HcQueue q = {0u, 0u, 0, n};
@@ -629,7 +660,10 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool pr
     if (ip >= wend) {  // 64 positions settled in parallel, one per lane
       wbase = ip;
       wend = ip + 64;
+      HC_T0();
       wmiss = ballot(hc_sure_miss(b, ip + b.lane, mflimit));
+      HC_ADD(6);
+      HC_CNT(7, 1);
     }
     const uint64_t run = ~(wmiss >> (ip - wbase));
     if (!(run & 1u)) {  // the reference steps ip++ over each of these (lz4hc.c:568)
@@ -719,8 +753,10 @@ __device__ int hc_compress_block(const HcBlock &b, uintptr_t dst, int n, bool pr
   }
 #ifdef RDK_HC_PROF
   if (b.lane == 0 && blockIdx.x < 4)
-    printf("HCPROF blk %d n %d build_us %.1f parse_us %.1f skipped %d out %d\n", int(blockIdx.x), n,
-           double(t1 - t0) / 100.0, double(wall_clock64() - t1) / 100.0, nskip, op);
+    printf("HCPROF blk %d n %d build_us %.1f parse_us %.1f skipped %d out %d | s1 cyc %llu n %llu | s2 cyc %llu n %llu | steps %llu serial %llu | miss cyc %llu n %llu\n", int(blockIdx.x), n,
+           double(t1 - t0) / 100.0, double(wall_clock64() - t1) / 100.0, nskip, op,
+           (unsigned long long)b.pc[0], (unsigned long long)b.pc[2], (unsigned long long)b.pc[1], (unsigned long long)b.pc[3],
+           (unsigned long long)b.pc[4], (unsigned long long)b.pc[5], (unsigned long long)b.pc[6], (unsigned long long)b.pc[7]);
 #endif
   return op;
 }

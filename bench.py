@@ -527,6 +527,101 @@ def bench_index(args, rank, world, n=None, per_batch=9500):
             "host_sample": (base, per_batch)}
 
 
+def bench_chain(args, rank, world, n=None, per_batch=9500):
+    """Both directions whole, every stage on the device and chained on one stream as a
+    broker thread would chain them, over ~1 MiB batches of ~100-byte JSON messages:
+      writer: record sizes + record writer (rdkafka_msgset_writer.c:652-754, :1117-1207)
+              -> LZ4F compress + header finalize + CRC32C (rdkafka_msgset_writer.c:1229-1335)
+      reader: CRC32C verify (rdkafka_msgset_reader.c:982-1015) -> LZ4F decompress
+              (rdkafka_msgset_reader.c:393-407) -> record index (rdkafka_msgset_reader.c:715-927)
+    Returns (writer result, reader result); the reader runs on the writer's batches, and the
+    rows it ends with are compared with the messages the writer began with."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import librdkafka_amd as L
+    n = n or args.partitions
+    base, d, payload = tiled_messages(n, per_batch, seed=42 + rank)
+    b = np.zeros(n, dtype=L.V2_BATCH_DTYPE)
+    b["first_msg"] = np.arange(n) * per_batch
+    b["msg_count"] = per_batch
+    b["producer_id"] = -1
+    b["base_sequence"] = -1
+    b["producer_epoch"] = -1
+    sets, offs, sizes, _ = L.msgset_v2_build(d, b, crc=False)
+    m = L._Msgs(*(d[k].data_ptr() for k in ("arena", "ts", "key_off", "key_len", "val_off",
+                                            "val_len", "hdr_off", "hdr_len", "hdr_cnt")))
+    rec_pos = torch.empty(n * per_batch, dtype=torch.int32, device="cuda")
+    max_ts = torch.empty(n, dtype=torch.int64, device="cuda")
+    rec_offs, rec_lens = offs + 61, sizes - 61
+    rl = rec_lens.cpu().numpy().astype(np.int64)
+    cap = (61 + L.lz4f_compress_bound(int(rl.max())) + 255) // 256 * 256
+    out = torch.empty(n * cap + 256, dtype=torch.uint8, device="cuda")
+    out_offs = torch.arange(n, dtype=torch.int64, device="cuda") * cap
+    out_caps = torch.full((n,), cap, dtype=torch.int32, device="cuda")
+    flens, blens, crcs = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    s = L._stream(None)
+    lib = L.lib()
+
+    def write_step():
+        lib.rdk_hip_msgset_v2_sizes(C.byref(m), b.ctypes.data, n, L._ptr(rec_pos), L._ptr(sizes),
+                                    L._ptr(max_ts), s)
+        lib.rdk_hip_msgset_v2_write(C.byref(m), b.ctypes.data, n, L._ptr(rec_pos), L._ptr(sizes),
+                                    L._ptr(max_ts), L._ptr(offs), L._ptr(sets), None, s)
+        L.msgset_v2_finalize(sets, rec_offs, rec_lens, out, out_offs, out_caps, flens, blens, crcs,
+                             mode=L.PRODUCER_EXACT)
+
+    wms, wkms = _timed(write_step, args.steps, args.warmup, world)
+    if not bool((blens == flens + 61).all()):
+        raise SystemExit(f"rank {rank}: a JSON batch was left uncompressed")
+    total = int(rl.sum())
+    clen = int(flens.to(torch.int64).sum())
+    writer = {"ms": wms, "kernel_ms": wkms, "bytes": total, "records": n,
+              # messages read (metadata + payload), MessageSets written, then read by the
+              # compressor, frames written, headers read + written
+              "alg_bytes": payload + 48 * n * per_batch + 2 * (total + 61 * n) + clen + 2 * 61 * n,
+              "ratio": total / clen}
+    # ---- reader over the finished batches
+    dslot = (int(rl.max()) + 255) // 256 * 256
+    dec = torch.empty(n * dslot + 256, dtype=torch.uint8, device="cuda")
+    doffs = torch.arange(n, dtype=torch.int64, device="cuda") * dslot
+    dcaps = torch.full((n,), dslot, dtype=torch.int32, device="cuda")
+    dl, st, vst, cnt = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(4))
+    pay_offs = out_offs + 61
+    row_offs = torch.arange(n, dtype=torch.int64, device="cuda") * per_batch
+    row_caps = torch.full((n,), per_batch, dtype=torch.int32, device="cuda")
+    rows = {k: torch.empty(n * per_batch, dtype=getattr(torch, t), device="cuda")
+            for k, t in L.V2_ROW_FIELDS}
+
+    def read_step():
+        L.msgset_v2_crc(out, out_offs, out_caps, vst, L.V2_CRC_VERIFY)
+        L.lz4f_decompress_batch(out, pay_offs, flens, dec, doffs, dcaps, dl, st)
+        L.msgset_v2_index(out, out_offs, dec, doffs, dl, row_offs, row_caps, rows, cnt)
+
+    rms, rkms = _timed(read_step, args.steps, args.warmup, world)
+    if int(vst.abs().sum()) or int(st.abs().sum()) or not bool((dl == rec_lens).all()) or \
+            not bool((cnt == per_batch).all()):
+        raise SystemExit(f"rank {rank}: the reader rejected the writer's batches")
+    # the rows against the messages: timestamps and value lengths of every record, value
+    # bytes of the first batch
+    if not torch.equal(rows["timestamp"], d["ts"]) or not torch.equal(rows["val_len"], d["val_len"]):
+        raise SystemExit(f"rank {rank}: rows differ from the messages")
+    arena = base["arena"]
+    r0 = {k: rows[k][:per_batch].cpu().numpy() for k in ("val_off", "val_len")}
+    d0 = dec[:dslot].cpu().numpy()
+    for j in range(0, per_batch, 97):
+        ln = int(r0["val_len"][j])
+        if ln > 0:
+            o = int(base["val_off"][j])
+            if bytes(d0[int(r0["val_off"][j]):int(r0["val_off"][j]) + ln]) != bytes(arena[o:o + ln]):
+                raise SystemExit(f"rank {rank}: row {j} value bytes differ from the message")
+    reader = {"ms": rms, "kernel_ms": rkms, "bytes": total, "records": n,
+              # batch read for the CRC, frame read + records written by the decoder, records
+              # + header read and 40 B of row written per record by the index
+              "alg_bytes": (clen + 61 * n) + clen + total + total + 61 * n + 40 * n * per_batch}
+    return writer, reader
+
+
 def bench_legacy(args, rank, world, n=None, set_bytes=1 << 20):
     """MsgVersion 1 MessageSets (~1 MiB of ~150-byte JSON messages each)
     through the consumer's per-message check.crcs (rd_kafka_msgset_reader_msg_v0_1,
@@ -1170,6 +1265,11 @@ def main():
             legs["v2_record_serialize_1MiB_json"] = serialize_leg(rank, world, no_cpu)
             legs["v2_record_index_1MiB_json"] = index_leg(rank, world, no_cpu)
             legs["v1_msgset_crc32_verify_1MiB_json"] = legacy_leg(rank, world, no_cpu)
+            wr, rd = bench_chain(sub, rank, world, n=256)
+            legs["writer_messages_to_batches_1MiB_json"] = leg_line(
+                "writer_messages_to_batches_1MiB_json", wr, 3, 1)
+            legs["reader_batches_to_rows_1MiB_json"] = leg_line(
+                "reader_batches_to_rows_1MiB_json", rd, 3, 1)
             legs["producer_pipeline_1MiB_json_pcie"] = leg_line(
                 "producer_pipeline_1MiB_json_pcie",
                 bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512), rank, world,

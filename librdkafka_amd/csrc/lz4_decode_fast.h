@@ -55,55 +55,69 @@ struct FastDec {
   lds_u8 *ring;      // kRing bytes of the newest output
   lds_u8 *map;       // 128 bytes: [0, 64) per-piece scratch, [64, 128) stores of parked lanes
   rsrc_t rin;        // compressed block [0, csize)
-  rsrc_t rout;       // block output [0, realcap)
+  g_u8 *out;         // block output; every position written or read lies below the checked end
   uint32_t csize;
   // the previous piece, fetched but not yet written: its HBM loads stay in
   // flight while the next piece's sources are worked out
   uint32_t pn, poc;  // live bytes (0: none) and output position
-  uint32_t plb, pfb, prb;
+  uint32_t plb, pfb, prb;  // the byte as each of the three sources delivered it
+  bool plit, prk;          // which one holds it: literal, history ring, else far history
 };
 
-// Write the pending piece into the history ring and to HBM.  Each lane's byte
-// arrived in exactly one of its three sources (parked loads read 0).
-// No branches: a lane without a byte stores into its parking slot / out of range.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m, uint32_t add) {
+  return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), add));
+}
+// value of lane `idx` (modulo 64), any lane pattern
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t idx) {
+  return uint32_t(__builtin_amdgcn_ds_bpermute(int(idx << 2), int(v)));
+}
+
+// Write the pending piece into the history ring and to HBM.
 __device__ __forceinline__ void fast_retire(FastDec &d, int lane) {
-  const bool live = uint32_t(lane) < d.pn;
-  const uint32_t v = d.plb | d.pfb | d.prb;
-  lds_u8 *slot = live ? d.ring + ((d.poc + uint32_t(lane)) & kRingMask) : d.map + 64 + lane;
-  *slot = uint8_t(v);
+  __builtin_amdgcn_sched_barrier(0);  // keep the wait for the piece's loads down here
+  // (the three values pass through empty asm statements: a select between fields of `d`
+  // would otherwise be turned into one load through a selected address, which puts the
+  // fields into scratch memory)
+  uint32_t a = d.plb, b = d.prb, c = d.pfb;
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
+  const uint32_t v = d.plit ? a : (d.prk ? b : c);
+  if (uint32_t(lane) < d.pn) {
+    d.ring[(d.poc + uint32_t(lane)) & kRingMask] = uint8_t(v);
+    d.out[d.poc + uint32_t(lane)] = uint8_t(v);
+  }
   asm volatile("" ::: "memory");
-  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), d.rout, live ? d.poc + uint32_t(lane) : kNoAccess,
-                                      0, 0);
   d.pn = 0;
 }
 
 // Fetch output bytes [pc, pc+nvalid): lane l's byte comes from `src` (kLitTag | input
-// position, or an output position below its own).  They are written by the next retire.
+// position, or an output position below its own; all ones in a lane without a byte).
+// They are written by the next retire.
 __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t src, uint32_t pc, uint32_t nvalid,
                                            int lane) {
   fast_retire(d, lane);  // the ring must hold everything before pc
-  const bool live = uint32_t(lane) < nvalid;
   // match sources inside this piece: pointer jumping, each step halves the
   // remaining hops (sources always point to lower lanes).  The shuffle is
   // unconditional: under a lane predicate its source lanes would read zeros.
   for (;;) {
-    // (a literal source has the tag bit set and compares below as a huge position: the
-    // signed compare keeps it out)
-    const bool intra = live & (int32_t(src) >= int32_t(pc));
+    // (a literal source has the tag bit set: the signed compare keeps it out)
+    const bool intra = int32_t(src) >= int32_t(pc);
     if (!fballot(intra)) break;
-    const uint32_t v = uint32_t(__shfl(int(src), int((src - pc) & 63u)));
+    const uint32_t v = lane_read(src, src - pc);
     src = intra ? v : src;
   }
   const bool lit = int32_t(src) < 0;
   const uint32_t q = src & ~kLitTag;
-  const bool ring_ok = !lit & (q + kRing >= pc);  // still in the history ring
-  const bool far = live & !lit & !ring_ok;
+  const bool rk = q + kRing >= pc;  // a match source still in the history ring
+  // a literal's position is in range of the input only with its tag taken off; a lane
+  // without a byte (all ones) stays out of range either way
+  d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, src ^ kLitTag, 0, 0);
   // far history was stored >= kRing/64 pieces (>= 64 vector-memory ops) ago:
   // with in-order vmcnt retirement it has completed, so no wait is needed
-  d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live & lit) ? q : kNoAccess, 0, 0);
-  d.pfb = __builtin_amdgcn_raw_buffer_load_b8(d.rout, far ? q : kNoAccess, 0, 0);
+  d.pfb = d.out[(lit | rk) ? 0u : q];
   asm volatile("" ::: "memory");  // ring bytes stored by other lanes
-  d.prb = d.ring[q & kRingMask] & (ring_ok ? 0xFFu : 0u);
+  d.prb = d.ring[q & kRingMask];
+  d.plit = lit;
+  d.prk = rk;
   d.pn = nvalid;
   d.poc = pc;
 }
@@ -274,9 +288,13 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
   d.ring = ring;
   d.map = map;
   d.rin = make_rsrc(src, csize);
-  d.rout = make_rsrc(dst, realcap);
+  // wave-uniform base: the output is addressed as scalar base + lane offset
+  d.out = (g_u8 *)(
+      (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(uint64_t(dst) >> 32)))) << 32) |
+      uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(dst)))));
   d.csize = csize;
   d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
+  d.plit = d.prk = false;
   const uint32_t olimit = realcap < 65536u ? realcap : 65536u;
   uint32_t op = 0, ipn = 0;
   // the last non-final sequence decides the end-of-block margins
@@ -307,7 +325,7 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
         const bool send = R & (J < 64u);
         const int t = __builtin_amdgcn_ds_permute(int((send ? J : x0) << 2), int(send));
         R = R | (t != 0);
-        const uint32_t jj = uint32_t(__shfl(int(J), int(J & 63u)));
+        const uint32_t jj = lane_read(J, J);
         J = J < 64u ? jj : 64u;
       }
       M = fballot(R);
@@ -356,32 +374,38 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
     }
     // ---- output [op, op+T) in pieces of 64 bytes, lane per byte
     const uint32_t op_new = uni(op + T);
-    const uint32_t f1 = ll | (off << 16);
-    const uint32_t f2 = (ostart & 0xFFFFu) | (ls << 16);  // a sequence with bytes starts < 65536
-    uint32_t carry = 0;  // member (lane + 1) whose bytes run into the piece
+    // the sequences that have bytes, packed into the low lanes in stream order (a sequence
+    // without bytes can only be the last one)
+    const uint64_t Mn = fballot(len != 0u);
+    const uint32_t slot = len != 0u ? lanes_below(Mn, 0u) : 63u;  // at most 22 sequences
+    const uint32_t f1 = uint32_t(__builtin_amdgcn_ds_permute(int(slot << 2), int(ll | (off << 16))));
+    // (a sequence with bytes starts below 65536)
+    const uint32_t f2 =
+        uint32_t(__builtin_amdgcn_ds_permute(int(slot << 2), int((ostart & 0xFFFFu) | (ls << 16))));
+    const uint32_t ost = len != 0u ? ostart : 0x80000000u;
+    uint32_t before = 0xFFFFFFFFu;  // sequences that start before the piece, less one
     for (uint32_t c = op; c < op_new; c = uni(c + 64u)) {
-      // member whose output starts at or before each lane's byte: starts in this piece are
-      // scattered into the map and max-scanned; lanes before the piece's first start take
-      // the member running into the piece (compiler barriers: other lanes' LDS stores are
-      // invisible to the optimizer, which would otherwise forward map[lane] = 0 to the read)
+      // sequence whose output starts at or before each lane's byte: the starts in this piece
+      // are scattered into the map; a lane's sequence is the count of starts up to its byte
+      // (compiler barriers: other lanes' LDS stores are invisible to the optimizer, which
+      // would otherwise forward map[lane] = 0 to the read)
       map[lane] = 0;
       asm volatile("" ::: "memory");
-      const uint32_t rel0 = ostart - c;
-      map[((len != 0u) & (rel0 < 64u)) ? rel0 : 64u + uint32_t(lane)] = uint8_t(lane + 1);
+      const uint32_t rel0 = ost - c;
+      map[rel0 < 64u ? rel0 : 64u + uint32_t(lane)] = 1;
       asm volatile("" ::: "memory");
-      uint32_t v = wave_incl_max(map[lane]);
-      v = v ? v : carry;
-      carry = __builtin_amdgcn_readlane(v, 63);
-      const int idx = int((v - 1u) & 63u);
-      const uint32_t g1 = uint32_t(__shfl(int(f1), idx));
-      const uint32_t g2 = uint32_t(__shfl(int(f2), idx));
+      const uint64_t sb = fballot(map[lane] != 0);
+      const uint32_t idx = lanes_below(sb >> 1, uni(before + uint32_t(sb & 1ull)));
+      before = uni(before + uint32_t(__builtin_popcountll(sb)));
+      const uint32_t g1 = lane_read(f1, idx);
+      const uint32_t g2 = lane_read(f2, idx);
       const uint32_t o = c + uint32_t(lane);
       const uint32_t rel = (o - g2) & 0xFFFFu;
       const uint32_t s_lit = ((g2 >> 16) + rel) | kLitTag, s_mat = o - (g1 >> 16);
-      const uint32_t pick = 0u - uint32_t(rel < (g1 & 0xFFFFu));  // all ones: a literal byte
-      const uint32_t s = (s_lit & pick) | (s_mat & ~pick);
+      const uint32_t s = rel < (g1 & 0xFFFFu) ? s_lit : s_mat;
       const uint32_t left = op_new - c;
-      fast_flush(d, s, c, left < 64u ? left : 64u, lane);
+      const uint32_t nv = left < 64u ? left : 64u;
+      fast_flush(d, uint32_t(lane) < nv ? s : 0xFFFFFFFFu, c, nv, lane);
     }
     op = op_new;
     if (done) {

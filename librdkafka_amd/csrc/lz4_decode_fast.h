@@ -144,6 +144,9 @@ struct SegHead {
   bool bad, complex;
 };
 
+// CHECKED = false: for a segment whose last candidate ends its length bytes before the
+// limits below (seg + 63 + 4 < csize - 15), where none of them can trip
+template <bool CHECKED = true>
 __device__ __forceinline__ SegHead seg_head(seg_u2 h, uint32_t csize, uint32_t seg, int lane) {
   const uint32_t p = seg + uint32_t(lane);
   const uint32_t w0 = __builtin_amdgcn_alignbyte(h.y, h.x, p & 3u);
@@ -161,8 +164,8 @@ __device__ __forceinline__ SegHead seg_head(seg_u2 h, uint32_t csize, uint32_t s
   // ip >= iend-15 stops the reference's loop early (loop_error, tolerated for literals)
   // where this parse would go on
   const uint32_t lim = csize - 15u;
-  r.bad = (e0 & ((p + 1u >= lim) | (csize < 16u))) | (e1 & (p + 2u >= lim)) |
-          (e2 & (p + 3u >= lim)) | (e3 & (p + 4u >= lim)) | (p >= csize);
+  r.bad = CHECKED && ((e0 & ((p + 1u >= lim) | (csize < 16u))) | (e1 & (p + 2u >= lim)) |
+                      (e2 & (p + 3u >= lim)) | (e3 & (p + 4u >= lim)) | (p >= csize));
   r.complex = e3;
   r.ll = ll;
   r.lit_end = p + r.k + ll;
@@ -306,32 +309,37 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
   // before this segment is expanded; the head bytes of seg+128 are in flight
   seg_u2 h2 = seg_load_head(d.rin, 64u, lane);
   for (;;) {
-    const SegHead nhd = seg_head(h2, csize, seg + 64u, lane);
+    const SegHead nhd = seg + 64u + 63u + 4u + 15u < csize
+                            ? seg_head<false>(h2, csize, seg + 64u, lane)
+                            : seg_head<true>(h2, csize, seg + 64u, lane);
     const seg_u2 ng = seg_load_tail(d.rin, nhd);
     h2 = seg_load_head(d.rin, seg + 128u, lane);
     // ---- walk: which candidate lanes are the real sequences of this segment
     const uint32_t x0 = ipn - seg;
     uint64_t M;
+    bool mem;
     for (;;) {
       // bad, complex, leaves the segment, or ends the block (nothing may follow csize)
       const bool stop = (cur.A - seg >= 64u) | (cur.A == csize);
       uint32_t J = stop ? 64u : cur.A - seg;
       bool R = uint32_t(lane) == x0;
       // One level: every reached lane marks its successor (a forward permute is a scatter;
-      // lanes that mark nothing send a zero to the entry lane, which nothing else targets
-      // and which is reached anyway), then the successor map is squared.
+      // lanes that mark nothing mark the entry lane, which nothing else targets and which
+      // is reached anyway), then the successor map is squared.
 #pragma unroll
       for (int level = 0; level < 5; ++level) {
         const bool send = R & (J < 64u);
-        const int t = __builtin_amdgcn_ds_permute(int((send ? J : x0) << 2), int(send));
+        const int t = __builtin_amdgcn_ds_permute(int((send ? J : x0) << 2), 1);
         R = R | (t != 0);
         const uint32_t jj = lane_read(J, J);
         J = J < 64u ? jj : 64u;
       }
       M = fballot(R);
-      if (fballot(R & (cur.A == kSeqBad))) return kFastFallback;
-      const uint64_t cx = fballot(R & (cur.A == kSeqComplex));
+      mem = R;
+      const uint32_t ra = R ? cur.A : 0u;
+      const uint64_t cx = fballot(ra >= kSeqBad);  // kSeqBad or kSeqComplex among the members
       if (!cx) break;
+      if (fballot(ra == kSeqBad)) return kFastFallback;
       // header too long for the lane's bytes: parse it scalar, then walk again
       const uint32_t xc = uint32_t(__builtin_ctzll(cx));
       const SegCand sc = seq_slow(d.rin, csize, seg + xc);
@@ -345,15 +353,16 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
     const uint32_t a_last = uni(__builtin_amdgcn_readlane(cur.A, xl));
     const bool done = a_last == csize;  // nothing can follow: the literals-only last sequence
     // ---- the segment's sequences, one per member lane, in lane order
-    const bool mem = (M >> lane) & 1ull;
     const uint32_t ll = cur.B & 0xFFFFu, ml = cur.B >> 16, off = cur.C & 0xFFFFu;
     const uint32_t ls = seg + uint32_t(lane) + (cur.C >> 16);
     uint32_t T;
     const uint32_t len = mem ? ll + ml : 0u;
     const uint32_t ostart = op + wave_excl_sum(len, T);
     const uint32_t cpy = ostart + ll;
-    const bool mm = mem & (ml != 0u);
-    if (fballot(mm & (off > cpy))) return kFastFallback;  // match < lowPrefix
+    // (ballots straight from one compare each: a ballot of a combined predicate goes
+    // through a 0/1 register)
+    const bool mm = (mem ? ml : 0u) != 0u;
+    if (fballot((mm ? off : 0u) > cpy)) return kFastFallback;  // match < lowPrefix
     if (op + T > olimit) return kFastFallback;  // the exact path reports the size error
     const uint64_t nl = fballot(mm);
     if (nl) {

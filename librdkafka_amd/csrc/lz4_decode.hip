@@ -483,7 +483,7 @@ lz4f_blocks_kernel(
     const uint64_t *__restrict__ out_offs, const uint32_t *__restrict__ out_caps, uint32_t n,
     const FrameState *__restrict__ fs, BlockDesc *__restrict__ bd,
     const uint32_t *__restrict__ work_count, const uint32_t *__restrict__ work) {
-  __shared__ __attribute__((aligned(16))) uint8_t rings[kDecWaves][kRing];
+  __shared__ __attribute__((aligned(kRing))) uint8_t rings[kDecWaves][kRing];  // (ring_at)
   __shared__ __attribute__((aligned(16))) uint8_t maps[kDecWaves][128];
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void lz4f_seq_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
     const uint32_t *__restrict__ out_caps, uint32_t n, FrameState *__restrict__ fs) {
-  __shared__ __attribute__((aligned(16))) uint8_t rings[kDecWaves][kRing];
+  __shared__ __attribute__((aligned(kRing))) uint8_t rings[kDecWaves][kRing];  // (ring_at)
   __shared__ __attribute__((aligned(16))) uint8_t maps[kDecWaves][128];
   const int lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;

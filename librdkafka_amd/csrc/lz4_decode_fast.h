@@ -64,6 +64,12 @@ struct FastDec {
   bool plit, prk;          // which one holds it: literal, history ring, else far history
 };
 
+// ring byte of output position x (the ring starts at a multiple of its size in LDS, so the
+// position's low bits are ORed into the base)
+__device__ __forceinline__ lds_u8 *ring_at(const FastDec &d, uint32_t x) {
+  return (lds_u8 *)(uintptr_t)(uint32_t(uintptr_t(d.ring)) | (x & kRingMask));
+}
+
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m, uint32_t add) {
   return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), add));
 }
@@ -82,8 +88,9 @@ __device__ __forceinline__ void fast_retire(FastDec &d, int lane) {
   asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
   const uint32_t v = d.plit ? a : (d.prk ? b : c);
   if (uint32_t(lane) < d.pn) {
-    d.ring[(d.poc + uint32_t(lane)) & kRingMask] = uint8_t(v);
-    d.out[d.poc + uint32_t(lane)] = uint8_t(v);
+    const uint32_t o = d.poc + uint32_t(lane);
+    *ring_at(d, o) = uint8_t(v);
+    d.out[o] = uint8_t(v);
   }
   asm volatile("" ::: "memory");
   d.pn = 0;
@@ -94,7 +101,6 @@ __device__ __forceinline__ void fast_retire(FastDec &d, int lane) {
 // They are written by the next retire.
 __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t src, uint32_t pc, uint32_t nvalid,
                                            int lane) {
-  fast_retire(d, lane);  // the ring must hold everything before pc
   // match sources inside this piece: pointer jumping, each step halves the
   // remaining hops (sources always point to lower lanes).  The shuffle is
   // unconditional: under a lane predicate its source lanes would read zeros.
@@ -105,6 +111,7 @@ __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t src, uint32_t pc
     const uint32_t v = lane_read(src, src - pc);
     src = intra ? v : src;
   }
+  fast_retire(d, lane);  // the ring must hold everything before pc
   const bool lit = int32_t(src) < 0;
   const uint32_t q = src & ~kLitTag;
   const bool rk = q + kRing >= pc;  // a match source still in the history ring
@@ -115,7 +122,7 @@ __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t src, uint32_t pc
   // with in-order vmcnt retirement it has completed, so no wait is needed
   d.pfb = d.out[(lit | rk) ? 0u : q];
   asm volatile("" ::: "memory");  // ring bytes stored by other lanes
-  d.prb = d.ring[q & kRingMask];
+  d.prb = *ring_at(d, q);
   d.plit = lit;
   d.prk = rk;
   d.pn = nvalid;
@@ -321,22 +328,23 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
     for (;;) {
       // bad, complex, leaves the segment, or ends the block (nothing may follow csize)
       const bool stop = (cur.A - seg >= 64u) | (cur.A == csize);
-      uint32_t J = stop ? 64u : cur.A - seg;
+      // successor lane as a permute address (lane * 4); 256: none
+      uint32_t J = stop ? 256u : (cur.A - seg) << 2;
       bool R = uint32_t(lane) == x0;
       // One level: every reached lane marks its successor (a forward permute is a scatter;
       // lanes that mark nothing mark the entry lane, which nothing else targets and which
       // is reached anyway), then the successor map is squared.
 #pragma unroll
       for (int level = 0; level < 5; ++level) {
-        const bool send = R & (J < 64u);
-        const int t = __builtin_amdgcn_ds_permute(int((send ? J : x0) << 2), 1);
+        const bool send = R & (J < 256u);
+        const int t = __builtin_amdgcn_ds_permute(int(send ? J : x0 << 2), 1);
         R = R | (t != 0);
-        const uint32_t jj = lane_read(J, J);
-        J = J < 64u ? jj : 64u;
+        const uint32_t jj = uint32_t(__builtin_amdgcn_ds_bpermute(int(J), int(J)));
+        J = J < 256u ? jj : 256u;
       }
-      M = fballot(R);
       mem = R;
       const uint32_t ra = R ? cur.A : 0u;
+      M = fballot(ra != 0u);  // (a member's A is never 0)
       const uint64_t cx = fballot(ra >= kSeqBad);  // kSeqBad or kSeqComplex among the members
       if (!cx) break;
       if (fballot(ra == kSeqBad)) return kFastFallback;
@@ -404,10 +412,11 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
       map[rel0 < 64u ? rel0 : 64u + uint32_t(lane)] = 1;
       asm volatile("" ::: "memory");
       const uint64_t sb = fballot(map[lane] != 0);
-      const uint32_t idx = lanes_below(sb >> 1, uni(before + uint32_t(sb & 1ull)));
+      const int idx4 =
+          int((lanes_below(sb >> 1, 0u) << 2) + uni((before + uint32_t(sb & 1ull)) << 2));
       before = uni(before + uint32_t(__builtin_popcountll(sb)));
-      const uint32_t g1 = lane_read(f1, idx);
-      const uint32_t g2 = lane_read(f2, idx);
+      const uint32_t g1 = uint32_t(__builtin_amdgcn_ds_bpermute(idx4, int(f1)));
+      const uint32_t g2 = uint32_t(__builtin_amdgcn_ds_bpermute(idx4, int(f2)));
       const uint32_t o = c + uint32_t(lane);
       const uint32_t rel = (o - g2) & 0xFFFFu;
       const uint32_t s_lit = ((g2 >> 16) + rel) | kLitTag, s_mat = o - (g1 >> 16);

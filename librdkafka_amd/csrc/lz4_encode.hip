@@ -542,32 +542,37 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
     for (int pos = em ? __builtin_ctzll(em) : 64; pos < 64; pos = __builtin_amdgcn_readlane(J0, pos))
       ch |= 1ull << pos;
     // per lane: the end of the previous chosen match (0: none).  Chosen matches do not
-    // overlap, so their ends grow with the lane: a running maximum, shifted by one lane
-    const bool isch = (ch >> lane) & 1ull;
-    const int pend = wave_excl_max(isch ? i + len : 0);
-    const bool lowc = pend != 0;
-    const bool interior = lowc && pend > i;
-    const uint64_t Mv = ballot(lane >= e && !interior);
-    uint64_t Tm = ballot(lowc && pend == i);
-    uint64_t Rm = ballot(lowc && pend == i + 2 && pend - w0 < 64);
+    // overlap, so their ends grow with the lane: a running maximum, shifted by one lane.
+    // The tests below are one vector compare each; their lane masks are combined on the
+    // scalar unit (a ballot of a combined predicate goes through a 0/1 register).
+    const bool isch = __builtin_amdgcn_inverse_ballot_w64(ch);
+    const int mend = i + len;
+    const int pend = wave_excl_max(isch ? mend : 0);
+    // (a match never ends at position 0, and pend == i + 2 puts the re-test inside the
+    // window exactly for lanes below 62)
+    const uint64_t Mv = ballot(pend <= i) & (~0ull << e);  // not inside a chosen match
+    uint64_t Tm = ballot(pend == i) & ~uint64_t(w0 == 0);
+    uint64_t Rm = ballot(pend == i + 2) & bits_below(62);
     if (mode == W_POSTMATCH) {
       Tm |= 4ull;
       Rm |= 1ull;
     }
     const uint64_t ins = Mv | Rm;
-    const int prev = lowc ? pend : anchor_in;
+    const int prev = pend > anchor_in ? pend : anchor_in;  // (a chosen end lies behind the anchor)
     const int blim = i - prev < tc ? i - prev : tc;  // lz4.c:958: ip>anchor, match>lowLimit
     const int fbk = bkr < blim ? bkr : blim;
-    const bool bad = (isch && ((bkr == kRegBack && blim > kRegBack) || sat || i + len >= b.mfl1)) ||
-                     (((Mv >> lane) & 1ull) && (eq & ins & ((1ull << lane) - 1ull)));
+    const uint64_t Blong = ballot(bkr == kRegBack) & ballot(blim > kRegBack);
+    const uint64_t Bsat = ballot(sat), Bend = ballot(mend >= b.mfl1);
+    const uint64_t Bdup = ballot((eq & ins & ((1ull << lane) - 1ull)) != 0);
+    const uint64_t badm = (ch & (Blong | Bsat | Bend)) | (Mv & Bdup);
     const int x1 = ch ? __builtin_ctzll(ch) : 63;
 #ifdef RDK_WIN_PROF
-    if (ballot(isch && (bkr == kRegBack && blim > kRegBack))) b.pt[7] += 1;
-    if (ballot(isch && sat)) b.pt[7] += 1ull << 16;
-    if (ballot(((Mv >> lane) & 1ull) && (eq & ins & ((1ull << lane) - 1ull)))) b.pt[7] += 1ull << 32;
+    if (ch & Blong) b.pt[7] += 1;
+    if (ch & Bsat) b.pt[7] += 1ull << 16;
+    if (Mv & Bdup) b.pt[7] += 1ull << 32;
     if (mode == W_SEARCH && b.cnt + x1 > 64) b.pt[7] += 1ull << 48;
 #endif
-    if (!ballot(bad) && !(mode == W_SEARCH && b.cnt + x1 > 64)) {
+    if (!badm && !(mode == W_SEARCH && b.cnt + x1 > 64)) {
       fast_done = true;
       seq_prev = prev;
       INS = ins;
@@ -701,7 +706,7 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   // ------------------------------------------------------------ table update
   // every inserted lane; the latest position per hash wins
   if (st != W_LAST) {
-    const bool ins = (INS >> lane) & 1ull;
+    const bool ins = __builtin_amdgcn_inverse_ballot_w64(INS);
     const uint64_t later = eq & INS & ~bits_below(lane + 1);
     if (ins && !later) table[h] = uint16_t(i);
     asm volatile("" ::: "memory");
@@ -711,10 +716,10 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   // A window holds a handful of sequences, far fewer than lanes: they are queued, one per
   // lane of the queue registers, and written out 64 at a time (flush_sequences).
   {
-    const bool ch = (chosen >> lane) & 1ull;
-    const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
+    const bool ch = __builtin_amdgcn_inverse_ballot_w64(chosen);
     int prev = seq_prev;  // this sequence's anchor (the parallel walk has it already)
     if (!fast_done) {
+      const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
       const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
       const int pend = __shfl(i + L_len, pl);  // end of the previous chosen match
       prev = lowc ? pend : anchor_in;
@@ -727,7 +732,9 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
       if (b.qn + cnt > 64 && flush_sequences(b, lane)) return W_OVERFLOW;
       // chosen lane -> queue lane qn + its rank among the chosen lanes: a forward permute
       // (scatter); the other lanes send to a lane outside the accepted range
-      const int tgt = ch ? b.qn + __builtin_popcountll(lowc) : ((b.qn + cnt) & 63);
+      const int rank = int(__builtin_amdgcn_mbcnt_hi(uint32_t(chosen >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(uint32_t(chosen), 0u)));
+      const int tgt = ch ? b.qn + rank : ((b.qn + cnt) & 63);
       const uint32_t r0 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(uint32_t(prev) | (lit << 16))));
       const uint32_t r1 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(off | (mc << 16))));
       const bool acc = lane >= b.qn && lane < b.qn + cnt;

@@ -417,7 +417,13 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   // the bytes a lane compares when it measures a match past its register window
   while (b.H < w0 + int(b.sa) + 64 + kMaxLen + 8) ring_fill(b, lane);
   uint32_t xd[9], yt[9];
-  ring_load9(b, (uint32_t(i) + b.sa) & ~3u, xd);
+  // (the window's 64 lanes read consecutive positions: all straight unless the window
+  // straddles the end of the ring, one window in ~40)
+  const uint32_t wb = (uint32_t(w0) + b.sa) & (kRingBytes - 1u);
+  if (wb >= 4u && wb + 64u + 32u <= kRingBytes)
+    ring_load9_straight(b, (uint32_t(i) + b.sa) & ~3u, xd);
+  else
+    ring_load9(b, (uint32_t(i) + b.sa) & ~3u, xd);
   const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
   const uint32_t seq = __builtin_amdgcn_alignbyte(xd[2], xd[1], shi);
   const uint32_t h = lz4_hash(seq);
@@ -426,8 +432,9 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   if (mode == W_FORCED && lane == 0) tc = forced_cand;
   // the candidate's 36 bytes: from the ring when it is that recent, else from memory
   const uint32_t ac = (uint32_t(tc) + b.sa) & ~3u;
-  const bool far = act && int(ac) - 4 < b.H - int(kRingBytes);
-  ring_load9(b, ac, yt);
+  // (a candidate whose 36 bytes run over an end of the ring is fetched like a far one)
+  const bool far = act && (int(ac) - 4 < b.H - int(kRingBytes) || !ring_straight(ac));
+  ring_load9_straight(b, ac, yt);
   // (issued for every window -- parked lanes touch no memory -- and consumed behind the
   // hash comparison below, which then runs while the gather is in flight)
   uint32_t g[9];

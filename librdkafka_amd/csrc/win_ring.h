@@ -72,6 +72,21 @@ __device__ __forceinline__ void ring_load9(const SrcRing &b, uint32_t a, uint32_
   }
 }
 
+// The same nine dwords for a lane whose window lies inside the ring without running over
+// either end (ring_straight(a)): one address, nine fixed offsets.  A lane for which that does
+// not hold reads LDS it has no use for (its address is kept inside the allocation).
+__device__ __forceinline__ bool ring_straight(uint32_t a) {
+  const uint32_t at = a & (kRingBytes - 1u);
+  return at - 4u <= kRingBytes - 36u - 4u;  // 4 <= at && at + 32 <= kRingBytes
+}
+__device__ __forceinline__ void ring_load9_straight(const SrcRing &b, uint32_t a, uint32_t d[9]) {
+  uint32_t at = a & (kRingBytes - 1u);
+  at = at < 4u ? 4u : at;
+  ring_lds_u32 *p = (ring_lds_u32 *)((ring_lds_u8 *)b.ring + (at - 4u));
+#pragma unroll
+  for (int k = 0; k < 9; ++k) d[k] = p[k];
+}
+
 __device__ __forceinline__ bool ring_has(const SrcRing &b, int v_lo, int v_hi) {  // [v_lo, v_hi)
   return v_lo >= b.H - int(kRingBytes) && v_hi <= b.H;
 }

@@ -450,13 +450,24 @@ __device__ __forceinline__ int window_step(WinBlock &b, int w0, int forced_cand,
   const bool tver = act && seq == __builtin_amdgcn_alignbyte(yt[2], yt[1], shc);
   const uint64_t VT = ballot(tver);
   RDK_PT(1);
-  int len = kRegLen;
+  // first differing bit behind the 4 hashed bytes: count of trailing zeros over dword pairs
+  // (64 when a pair is equal), chained arithmetically -- no compare-and-select per dword
+  uint32_t zz[6];
 #pragma unroll
-  for (int k = 6; k >= 1; --k) {
-    const uint32_t z = __builtin_amdgcn_alignbyte(xd[k + 2], xd[k + 1], shi) ^
-                       __builtin_amdgcn_alignbyte(yt[k + 2], yt[k + 1], shc);
-    if (z) len = 4 * k + (__builtin_ctz(z) >> 3);
+  for (int k = 1; k <= 6; ++k)
+    zz[k - 1] = __builtin_amdgcn_alignbyte(xd[k + 2], xd[k + 1], shi) ^
+                __builtin_amdgcn_alignbyte(yt[k + 2], yt[k + 1], shc);
+  uint32_t cz[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint64_t w = (uint64_t(zz[2 * k + 1]) << 32) | zz[2 * k];
+    cz[k] = w ? uint32_t(__builtin_ctzll(w)) : 64u;
   }
+  // (a pair's count is 64 exactly when the pair is equal: only then the next pair counts)
+  uint32_t fd = cz[1] + (cz[1] >> 6) * cz[2];
+  fd = cz[0] + (cz[0] >> 6) * fd;
+  fd >>= 3;
+  int len = 4 + int(fd < uint32_t(kRegLen - 4) ? fd : uint32_t(kRegLen - 4));
   // a match that fills the register window is measured on from the ring, 4 bytes a step, up
   // to kMaxLen; `sat` = the length is still not final (kMaxLen reached, or a candidate older
   // than the ring) and has to be finished from memory if the parse takes this match

@@ -179,13 +179,21 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
                      __builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi) ==
                          __builtin_amdgcn_alignbyte(y.t[2], y.t[1], shc);
   const uint64_t vm = ballot(valid);
-  int len = kFastLen;
+  // first differing bit behind the 4 verified bytes: trailing-zero counts over dword pairs
+  // (64 exactly when a pair is equal: only then the next pair counts)
+  uint32_t cz[3];
 #pragma unroll
-  for (int k = 6; k >= 1; --k) {
-    const uint32_t z = __builtin_amdgcn_alignbyte(x.d[k + 2], x.d[k + 1], shi) ^
-                       __builtin_amdgcn_alignbyte(y.t[k + 2], y.t[k + 1], shc);
-    if (z) len = 4 * k + (__builtin_ctz(z) >> 3);
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t z0 = __builtin_amdgcn_alignbyte(x.d[2 * k + 3], x.d[2 * k + 2], shi) ^
+                        __builtin_amdgcn_alignbyte(y.t[2 * k + 3], y.t[2 * k + 2], shc);
+    const uint32_t z1 = __builtin_amdgcn_alignbyte(x.d[2 * k + 4], x.d[2 * k + 3], shi) ^
+                        __builtin_amdgcn_alignbyte(y.t[2 * k + 4], y.t[2 * k + 3], shc);
+    const uint64_t w = (uint64_t(z1) << 32) | z0;
+    cz[k] = w ? uint32_t(__builtin_ctzll(w)) : 64u;
   }
+  uint32_t fd = cz[1] + (cz[1] >> 6) * cz[2];
+  fd = (cz[0] + (cz[0] >> 6) * fd) >> 3;
+  int len = 4 + int(fd < uint32_t(kFastLen - 4) ? fd : uint32_t(kFastLen - 4));
   if (len > b.mlim - i) len = b.mlim - i;
 
   // greedy walk: first verified position at or after the end of the last match
@@ -213,7 +221,7 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
   // sequence fields of the chosen lanes.  Every round runs the same store
   // instructions (parked lanes write nothing), so the vmcnt bookkeeping never
   // depends on how many sequences a round produced.
-  const bool ch = (chosen >> lane) & 1ull;
+  const bool ch = __builtin_amdgcn_inverse_ballot_w64(chosen);
   const uint64_t below = chosen & ((1ull << lane) - 1ull);
   const int pl = below ? 63 - __builtin_clzll(below) : lane;
   const int pend = __shfl(lane + len, pl);       // end of the previous chosen match
@@ -233,7 +241,9 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
     if (b.qn + cnt > 64 && !flush_sequences(b, lane)) return false;
     // chosen lane -> queue lane qn + its rank among the chosen lanes: a forward permute
     // (scatter); the other lanes send to a lane outside the accepted range
-    const int tgt = ch ? b.qn + __builtin_popcountll(below) : ((b.qn + cnt) & 63);
+    const int rank = int(__builtin_amdgcn_mbcnt_hi(uint32_t(chosen >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo(uint32_t(chosen), 0u)));
+    const int tgt = ch ? b.qn + rank : ((b.qn + cnt) & 63);
     const uint32_t r0 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(lstart | (lit << 16))));
     const uint32_t r1 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(off | (mc << 16))));
     const bool acc = lane >= b.qn && lane < b.qn + cnt;

@@ -390,7 +390,13 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
   const bool act = i < b.ip_limit;  // a probe here has next_ip <= ip_limit; a re-test has ip < ip_limit
   while (b.H < w0 + int(b.sa) + 64 + kSnMaxLen + 8) ring_fill(b, lane);
   uint32_t xd[9], yt[9];
-  ring_load9(b, (uint32_t(i) + b.sa) & ~3u, xd);
+  // (the window's 64 lanes read consecutive positions: all straight unless the window
+  // straddles the end of the ring)
+  const uint32_t wb = (uint32_t(w0) + b.sa) & (kRingBytes - 1u);
+  if (wb >= 4u && wb + 64u + 32u <= kRingBytes)
+    ring_load9_straight(b, (uint32_t(i) + b.sa) & ~3u, xd);
+  else
+    ring_load9(b, (uint32_t(i) + b.sa) & ~3u, xd);
   const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
   const uint32_t seq = __builtin_amdgcn_alignbyte(xd[2], xd[1], shi);
   const uint32_t h = (seq * kSnMul) >> b.shift;
@@ -398,8 +404,9 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
   if (mode == SN_FORCED && lane == 0) tc = forced_cand;
   // the candidate's 36 bytes: from the ring when it is that recent, else from memory
   const uint32_t ac = (uint32_t(tc) + b.sa) & ~3u;
-  const bool far = act && int(ac) - 4 < b.H - int(kRingBytes);
-  ring_load9(b, ac, yt);
+  // (a candidate whose 36 bytes run over an end of the ring is fetched like a far one)
+  const bool far = act && (int(ac) - 4 < b.H - int(kRingBytes) || !ring_straight(ac));
+  ring_load9_straight(b, ac, yt);
   // (issued for every window -- parked lanes touch no memory -- and consumed behind the
   // hash comparison below, which then runs while the gather is in flight)
   uint32_t g[9];
@@ -414,13 +421,21 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
   const uint32_t shc = (uint32_t(tc) + b.sa) & 3u;
   const bool tver = act && seq == __builtin_amdgcn_alignbyte(yt[2], yt[1], shc);
   const uint64_t VT = ballot(tver);
-  int len = kSnRegLen;
+  // first differing bit behind the 4 hashed bytes: trailing-zero counts over dword pairs
+  // (64 exactly when a pair is equal: only then the next pair counts)
+  uint32_t cz[3];
 #pragma unroll
-  for (int k = 6; k >= 1; --k) {
-    const uint32_t z = __builtin_amdgcn_alignbyte(xd[k + 2], xd[k + 1], shi) ^
-                       __builtin_amdgcn_alignbyte(yt[k + 2], yt[k + 1], shc);
-    if (z) len = 4 * k + (__builtin_ctz(z) >> 3);
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t z0 = __builtin_amdgcn_alignbyte(xd[2 * k + 3], xd[2 * k + 2], shi) ^
+                        __builtin_amdgcn_alignbyte(yt[2 * k + 3], yt[2 * k + 2], shc);
+    const uint32_t z1 = __builtin_amdgcn_alignbyte(xd[2 * k + 4], xd[2 * k + 3], shi) ^
+                        __builtin_amdgcn_alignbyte(yt[2 * k + 4], yt[2 * k + 3], shc);
+    const uint64_t w = (uint64_t(z1) << 32) | z0;
+    cz[k] = w ? uint32_t(__builtin_ctzll(w)) : 64u;
   }
+  uint32_t fd = cz[1] + (cz[1] >> 6) * cz[2];
+  fd = (cz[0] + (cz[0] >> 6) * fd) >> 3;
+  int len = 4 + int(fd < uint32_t(kSnRegLen - 4) ? fd : uint32_t(kSnRegLen - 4));
   // a match that fills the register window is measured on from the ring, 4 bytes a step, up
   // to kSnMaxLen; `sat` = the length is still not final and has to be finished from memory if
   // the parse takes this match
@@ -477,12 +492,14 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
       ch |= 1ull << pos;
     // per lane: the end of the previous chosen copy (0: none).  Chosen copies do not
     // overlap, so their ends grow with the lane: a running maximum, shifted by one lane
-    const int pend = wave_excl_max(((ch >> lane) & 1ull) ? i + len : 0);
-    const bool lowc = pend != 0;
-    const bool interior = lowc && pend > i;
-    const uint64_t Mv = ballot(lane >= e && !interior);
-    uint64_t Tm = ballot(lowc && pend == i);
-    uint64_t Rm = ballot(lowc && pend == i + 1 && pend - w0 < 64);
+    // (the tests below are one vector compare each; their lane masks are combined on the
+    // scalar unit.  A copy never ends at position 0, and pend == i + 1 puts the re-test
+    // inside the window exactly for lanes below 63.)
+    const int mend = i + len;
+    const int pend = wave_excl_max(__builtin_amdgcn_inverse_ballot_w64(ch) ? mend : 0);
+    const uint64_t Mv = ballot(pend <= i) & (~0ull << e);  // not inside a chosen copy
+    uint64_t Tm = ballot(pend == i) & ~uint64_t(w0 == 0);
+    uint64_t Rm = ballot(pend == i + 1) & bits_below(63);
     if (mode == SN_POSTMATCH) {
       Tm |= 2ull;
       Rm |= 1ull;
@@ -490,17 +507,17 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
     // probe index of every searched lane: its distance from the last re-tested lane
     const uint64_t lt = Tm & ((1ull << lane) - 1ull);
     const int idx = lt ? lane - 1 - (63 - __builtin_clzll(lt)) : b.cnt + lane;
-    const bool searched = ((Mv & ~Tm) >> lane) & 1ull;
-    const uint64_t over = ballot(searched && idx > kSnStride1 && !(mode == SN_FORCED && lane == 0));
+    const uint64_t over =
+        ballot(idx > kSnStride1) & Mv & ~Tm & ~uint64_t(mode == SN_FORCED);  // (FORCED: lane 0)
     const int Z = over ? __builtin_ctzll(over) : 64;
     ch &= bits_below(Z);
     const uint64_t ins = (Mv | Rm) & bits_below(Z);
-    const bool isch = (ch >> lane) & 1ull;
-    const bool bad = lane < Z && ((isch && (sat || i + len >= b.ip_limit)) ||
-                                  (((Mv >> lane) & 1ull) && (eq & ins & ((1ull << lane) - 1ull))));
-    if (!ballot(bad)) {
+    const uint64_t Bsat = ballot(sat), Bend = ballot(mend >= b.ip_limit);
+    const uint64_t Bdup = ballot((eq & ins & ((1ull << lane) - 1ull)) != 0);
+    const uint64_t badm = bits_below(Z) & ((ch & (Bsat | Bend)) | (Mv & Bdup));
+    if (!badm) {
       fast_done = true;
-      seq_prev = lowc ? pend : anchor_in;
+      seq_prev = pend > anchor_in ? pend : anchor_in;  // (a chosen end lies behind the anchor)
       INS = ins;
       chosen = ch;
       L_cand = tc;
@@ -642,7 +659,7 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
   // ------------------------------------------------------------ table update
   // every inserted lane; the latest position per hash wins
   if (st != SN_LAST) {
-    const bool ins = (INS >> lane) & 1ull;
+    const bool ins = __builtin_amdgcn_inverse_ballot_w64(INS);
     const uint64_t later = eq & INS & ~bits_below(lane + 1);
     if (ins && !later) table[h] = uint16_t(i);
     asm volatile("" ::: "memory");
@@ -651,10 +668,10 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
   // A window holds a handful of copies, far fewer than lanes: they are queued, one per lane
   // of the queue registers, and written out 64 at a time (sn_flush_elements).
   {
-    const bool ch = (chosen >> lane) & 1ull;
-    const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
+    const bool ch = __builtin_amdgcn_inverse_ballot_w64(chosen);
     int prev = seq_prev;  // where this copy's literal starts (the parallel walk has it already)
     if (!fast_done) {
+      const uint64_t lowc = chosen & ((1ull << lane) - 1ull);
       const int pl = lowc ? 63 - __builtin_clzll(lowc) : lane;
       const int pend = __shfl(i + L_len, pl);  // end of the previous chosen copy
       prev = lowc ? pend : anchor_in;
@@ -666,7 +683,9 @@ __device__ __forceinline__ int sn_window_step(SnFrag &b, int w0, int forced_cand
       if (b.qn + cnt > 64) sn_flush_elements(b, lane);
       // chosen lane -> queue lane qn + its rank among the chosen lanes: a forward permute
       // (scatter); the other lanes send to a lane outside the accepted range
-      const int tgt = ch ? b.qn + __builtin_popcountll(lowc) : ((b.qn + cnt) & 63);
+      const int rank = int(__builtin_amdgcn_mbcnt_hi(uint32_t(chosen >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(uint32_t(chosen), 0u)));
+      const int tgt = ch ? b.qn + rank : ((b.qn + cnt) & 63);
       const uint32_t r0 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(uint32_t(prev) | (lit << 16))));
       const uint32_t r1 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(off | (ml << 16))));
       const bool acc = lane >= b.qn && lane < b.qn + cnt;

@@ -865,40 +865,60 @@ struct SnDec {
   // rin spans the whole dwords that hold the stream (a range-checked dword that is only
   // partly inside a buffer reads as zero, and a stream may end in a 2-byte element):
   // offsets into it are stream positions + din
-  sn_rsrc_t rin, rout;
+  sn_rsrc_t rin;
+  g_u8 *out;  // output; every position written or read lies below the checked length
   uint32_t din;
-  uint32_t pn, poc, plb, pfb, prb;  // the fetched, not yet written piece
+  // the fetched, not yet written piece: the byte as each of the three sources delivered it,
+  // and which one holds it (literal, history ring, else far history)
+  uint32_t pn, poc, plb, pfb, prb;
+  bool plit, prk;
 };
 
+// a start position no piece below `end` contains
+__device__ __forceinline__ uint32_t c_none(uint32_t end) { return end + 0x40000000u; }
+
+__device__ __forceinline__ void sn_set_out(SnDec &d, uintptr_t dst) {
+  // wave-uniform base: the output is addressed as scalar base + lane offset
+  d.out = (g_u8 *)((uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(uint64_t(dst) >> 32)))) << 32) |
+                   uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(dst)))));
+}
+
 __device__ __forceinline__ void sn_retire(SnDec &d, int lane) {
-  const bool live = uint32_t(lane) < d.pn;
-  const uint32_t v = d.plb | d.pfb | d.prb;
-  sn_lds_u8 *slot = live ? d.ring + ((d.poc + uint32_t(lane)) & kSnRingMask) : d.map + 64 + lane;
-  *slot = uint8_t(v);
+  __builtin_amdgcn_sched_barrier(0);  // keep the wait for the piece's loads down here
+  // (through empty asm statements: a select between fields of `d` would otherwise become one
+  // load through a selected address, which puts the fields into scratch memory)
+  uint32_t a = d.plb, b = d.prb, c = d.pfb;
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
+  const uint32_t v = d.plit ? a : (d.prk ? b : c);
+  if (uint32_t(lane) < d.pn) {
+    const uint32_t o = d.poc + uint32_t(lane);
+    d.ring[o & kSnRingMask] = uint8_t(v);
+    d.out[o] = uint8_t(v);
+  }
   asm volatile("" ::: "memory");
-  __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), d.rout, live ? d.poc + uint32_t(lane) : kSnNoAccess, 0, 0);
   d.pn = 0;
 }
 
 // fetch output bytes [pc, pc+nvalid): lane l's byte comes from `src` (tag | input position, or
-// an output position below its own)
+// an output position below its own; all ones in a lane without a byte)
 __device__ __forceinline__ void sn_flush(SnDec &d, uint32_t src, uint32_t pc, uint32_t nvalid, int lane) {
-  sn_retire(d, lane);
-  const bool live = uint32_t(lane) < nvalid;
   for (;;) {  // sources inside the piece: pointer jumping (unconditional shuffle, then select)
-    const bool intra = live & (int32_t(src) >= int32_t(pc));
+    const bool intra = int32_t(src) >= int32_t(pc);  // (a tagged source is negative)
     if (!sn_ballot(intra)) break;
-    const uint32_t v = uint32_t(__shfl(int(src), int((src - pc) & 63u)));
+    const uint32_t v = uint32_t(__builtin_amdgcn_ds_bpermute(int((src - pc) << 2), int(src)));
     src = intra ? v : src;
   }
+  sn_retire(d, lane);  // the ring must hold everything before pc
   const bool lit = int32_t(src) < 0;
   const uint32_t q = src & ~kSnLitTag;
-  const bool ring_ok = !lit & (q + kSnRing >= pc);
-  const bool far = live & !lit & !ring_ok;
-  d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, (live & lit) ? q + d.din : kSnNoAccess, 0, 0);
-  d.pfb = __builtin_amdgcn_raw_buffer_load_b8(d.rout, far ? q : kSnNoAccess, 0, 0);
+  const bool rk = q + kSnRing >= pc;  // a copy source still in the history ring
+  // (a lane without a byte stays out of the input's range: positions are below 2^31 - din)
+  d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, lit ? q + d.din : kSnNoAccess, 0, 0);
+  d.pfb = d.out[(lit | rk) ? 0u : q];
   asm volatile("" ::: "memory");
-  d.prb = d.ring[q & kSnRingMask] & (ring_ok ? 0xFFu : 0u);
+  d.prb = d.ring[q & kSnRingMask];
+  d.plit = lit;
+  d.prk = rk;
   d.pn = nvalid;
   d.poc = pc;
 }
@@ -968,22 +988,29 @@ __device__ int sn_decode_elems(SnDec &d, uint32_t n, uint32_t ipn, uint32_t ulen
     // ---- walk: which candidate lanes are the real elements of this segment
     const uint32_t x0 = ipn - seg;
     uint64_t M;
+    bool mem;
     for (;;) {
       const bool stop = (cur.A - seg >= 64u) | (cur.A == n);  // bad, complex, leaves, or ends the stream
-      uint32_t J = stop ? 64u : cur.A - seg;
+      // successor lane as a permute address (lane * 4); 256: none.  A level marks every
+      // reached lane's successor (lanes that mark nothing mark the entry lane, which is
+      // reached anyway) and squares the successor map.
+      uint32_t J = stop ? 256u : (cur.A - seg) << 2;
       bool R = uint32_t(lane) == x0;
 #pragma unroll
       for (int level = 0; level < 5; ++level) {
-        const bool send = R & (J < 64u);
-        const int t = __builtin_amdgcn_ds_permute(int((send ? J : x0) << 2), int(send));
+        const bool send = R & (J < 256u);
+        const int t = __builtin_amdgcn_ds_permute(int(send ? J : x0 << 2), 1);
         R = R | (t != 0);
-        const uint32_t jj = uint32_t(__shfl(int(J), int(J & 63u)));
-        J = J < 64u ? jj : 64u;
+        const uint32_t jj = uint32_t(__builtin_amdgcn_ds_bpermute(int(J), int(J)));
+        J = J < 256u ? jj : 256u;
       }
-      M = sn_ballot(R);
-      if (sn_ballot(R & (cur.A == kSnBad))) return SN_FAIL(4);
-      const uint64_t cx = sn_ballot(R & (cur.A == kSnComplex));
+      mem = R;
+      // (ballots straight from one compare each; a member's A is never 0)
+      const uint32_t ra = R ? cur.A : 0u;
+      M = sn_ballot(ra != 0u);
+      const uint64_t cx = sn_ballot(ra >= kSnBad);  // kSnBad or kSnComplex among the members
       if (!cx) break;
+      if (sn_ballot(ra == kSnBad)) return SN_FAIL(4);
       // header with a fifth byte: literal of 2^24 bytes or more, or a 4-byte offset
       const uint32_t xc = uint32_t(__builtin_ctzll(cx));
       const uint32_t p = seg + xc;
@@ -1010,7 +1037,6 @@ __device__ int sn_decode_elems(SnDec &d, uint32_t n, uint32_t ipn, uint32_t ulen
     if (a_last > n) return SN_FAIL(6);  // the last literal runs past the input
     const bool done = a_last == n;
     // ---- the segment's elements, one per member lane, in lane order
-    const bool mem = (M >> lane) & 1ull;
     const uint32_t ll = cur.ll, ml = cur.mk & 0xFFu, off = cur.off, k = cur.mk >> 8;
     const uint32_t len = mem ? ll + ml : 0u;
     // (the members' literals are disjoint pieces of an input below 2^31 bytes, so the sum of
@@ -1019,32 +1045,45 @@ __device__ int sn_decode_elems(SnDec &d, uint32_t n, uint32_t ipn, uint32_t ulen
     const uint32_t ostart = op + sn_excl_sum(len, T);
     if (uint64_t(op) + T > ulen) return SN_FAIL(7);  // writer_append* : no room (:572, :543)
     // writer_append_from_self: offset 0 or beyond the produced bytes (:548)
-    if (sn_ballot(mem & (ml != 0u) & (ostart <= off - 1u))) return SN_FAIL(8);
+    if (sn_ballot((mem ? ml : 0u) != 0u) & sn_ballot(ostart <= off - 1u)) return SN_FAIL(8);
     // ---- output [op, op+T) in pieces of 64 bytes, lane per byte
     const uint32_t op_new = uni(op + T);
     const uint32_t ls = seg + uint32_t(lane) + k;  // first literal byte
-    uint32_t carry = 0;
+    // every member has bytes; their fields are packed into the low lanes in stream order (a
+    // segment holds at most 32 elements): first byte that is not a literal, literal position
+    // minus output position, copy offset
+    const uint64_t Mn = sn_ballot(len != 0u);
+    const uint32_t slot = len != 0u ? __builtin_amdgcn_mbcnt_hi(uint32_t(Mn >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo(uint32_t(Mn), 0u))
+                                    : 63u;
+    const uint32_t f_cpy = uint32_t(__builtin_amdgcn_ds_permute(int(slot << 2), int(ostart + ll)));
+    const uint32_t f_dl = uint32_t(__builtin_amdgcn_ds_permute(int(slot << 2), int(ls - ostart)));
+    const uint32_t f_of = uint32_t(__builtin_amdgcn_ds_permute(int(slot << 2), int(off)));
+    const uint32_t ost = len != 0u ? ostart : c_none(op_new);
+    uint32_t before = 0xFFFFFFFFu;  // elements that start before the piece, less one
     for (uint32_t c = op; c < op_new; c = uni(c + 64u)) {
+      // the starts in this piece are scattered into the map; a lane's element is the count of
+      // starts up to its byte
       map[lane] = 0;
       asm volatile("" ::: "memory");
-      const uint32_t rel0 = ostart - c;
-      map[((len != 0u) & (rel0 < 64u)) ? rel0 : 64u + uint32_t(lane)] = uint8_t(lane + 1);
+      const uint32_t rel0 = ost - c;
+      map[rel0 < 64u ? rel0 : 64u + uint32_t(lane)] = 1;
       asm volatile("" ::: "memory");
-      uint32_t v = sn_incl_max(map[lane]);
-      v = v ? v : carry;
-      carry = __builtin_amdgcn_readlane(v, 63);
-      const int idx = int((v - 1u) & 63u);
-      const uint32_t g_os = uint32_t(__shfl(int(ostart), idx));
-      const uint32_t g_ll = uint32_t(__shfl(int(ll), idx));
-      const uint32_t g_ls = uint32_t(__shfl(int(ls), idx));
-      const uint32_t g_of = uint32_t(__shfl(int(off), idx));
+      const uint64_t sb = sn_ballot(map[lane] != 0);
+      const uint64_t s1 = sb >> 1;
+      const uint32_t cntb = __builtin_amdgcn_mbcnt_hi(uint32_t(s1 >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(uint32_t(s1), 0u));
+      const int idx4 = int((cntb << 2) + uni((before + uint32_t(sb & 1ull)) << 2));
+      before = uni(before + uint32_t(__builtin_popcountll(sb)));
+      const uint32_t g_cpy = uint32_t(__builtin_amdgcn_ds_bpermute(idx4, int(f_cpy)));
+      const uint32_t g_dl = uint32_t(__builtin_amdgcn_ds_bpermute(idx4, int(f_dl)));
+      const uint32_t g_of = uint32_t(__builtin_amdgcn_ds_bpermute(idx4, int(f_of)));
       const uint32_t o = c + uint32_t(lane);
-      const uint32_t rel = o - g_os;
-      const uint32_t s_lit = (g_ls + rel) | kSnLitTag, s_mat = o - g_of;
-      const uint32_t pick = 0u - uint32_t(rel < g_ll);
-      const uint32_t s = (s_lit & pick) | (s_mat & ~pick);
+      const uint32_t s_lit = (o + g_dl) | kSnLitTag, s_mat = o - g_of;
+      const uint32_t s = o < g_cpy ? s_lit : s_mat;
       const uint32_t left = op_new - c;
-      sn_flush(d, s, c, left < 64u ? left : 64u, lane);
+      const uint32_t nv = left < 64u ? left : 64u;
+      sn_flush(d, uint32_t(lane) < nv ? s : 0xFFFFFFFFu, c, nv, lane);
     }
     op = op_new;
     if (done) {
@@ -1074,6 +1113,7 @@ __device__ int sn_decode_stream(uintptr_t src, uint32_t n, uintptr_t dst, uint32
   d.din = uint32_t(src & 3u);
   d.rin = sn_make_rsrc(src - d.din, (d.din + n + 3u) & ~3u);
   d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
+  d.plit = d.prk = false;
   // read_uncompressed_length (snappy.c:1193-1218)
   uint32_t ulen = 0, ip0 = 0;
   for (uint32_t shift = 0;; shift += 7u) {
@@ -1085,7 +1125,7 @@ __device__ int sn_decode_stream(uintptr_t src, uint32_t n, uintptr_t dst, uint32
   *ulen_out = ulen;
   if (ulen > 0x7FFFFFF0u) return SN_FAIL(3);  // positions are kept in 31 bits
   if (ulen > cap) return kSnDstSize;      // the caller sizes dst from the preamble
-  d.rout = sn_make_rsrc(dst, ulen);
+  sn_set_out(d, dst);
   return sn_decode_elems(d, n, ip0, ulen, map, lane);
 }
 
@@ -1113,8 +1153,9 @@ __device__ bool sn_scan_stream(uintptr_t src, uint32_t n, uint32_t cap, SnSplit 
   d.map = nullptr;
   d.din = uint32_t(src & 3u);
   d.rin = sn_make_rsrc(src - d.din, (d.din + n + 3u) & ~3u);
-  d.rout = d.rin;
+  d.out = nullptr;
   d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
+  d.plit = d.prk = false;
   uint32_t ulen = 0, ip0 = 0;
   for (uint32_t shift = 0;; shift += 7u) {
     if (shift >= 32u || ip0 >= n) return false;
@@ -1135,34 +1176,38 @@ __device__ bool sn_scan_stream(uintptr_t src, uint32_t n, uint32_t cap, SnSplit 
   for (;;) {
     const uint32_t x0 = ipn - seg;
     const bool stop = (cur.A - seg >= 64u) | (cur.A == n);
-    uint32_t J = stop ? 64u : cur.A - seg;
+    uint32_t J = stop ? 256u : (cur.A - seg) << 2;  // successor as a permute address; 256: none
     bool R = uint32_t(lane) == x0;
 #pragma unroll
     for (int level = 0; level < 5; ++level) {
-      const bool send = R & (J < 64u);
-      const int tt = __builtin_amdgcn_ds_permute(int((send ? J : x0) << 2), int(send));
+      const bool send = R & (J < 256u);
+      const int tt = __builtin_amdgcn_ds_permute(int(send ? J : x0 << 2), 1);
       R = R | (tt != 0);
-      const uint32_t jj = uint32_t(__shfl(int(J), int(J & 63u)));
-      J = J < 64u ? jj : 64u;
+      const uint32_t jj = uint32_t(__builtin_amdgcn_ds_bpermute(int(J), int(J)));
+      J = J < 256u ? jj : 256u;
     }
-    const uint64_t M = sn_ballot(R);
-    if (sn_ballot(R & ((cur.A == kSnBad) | (cur.A == kSnComplex)))) return false;
+    const bool mem = R;
+    const uint32_t ra = R ? cur.A : 0u;  // (a member's A is never 0)
+    const uint64_t M = sn_ballot(ra != 0u);
+    if (sn_ballot(ra >= kSnBad)) return false;  // kSnBad or kSnComplex
     const uint32_t xl = uint32_t(63 - __builtin_clzll(M));
     const uint32_t a_last = uni(__builtin_amdgcn_readlane(cur.A, xl));
     if (a_last > n) return false;
-    const bool mem = (M >> lane) & 1ull;
     const uint32_t ll = cur.ll, ml = cur.mk & 0xFFu, off = cur.off;
     const uint32_t len = mem ? ll + ml : 0u;
     uint32_t T;
     const uint32_t ostart = op + sn_excl_sum(len, T);
     if (uint64_t(op) + T > ulen) return false;
     const uint32_t in_frag = ostart & (kSnBlock - 1u);
-    const bool crosses = mem & (in_frag + len > kSnBlock);
-    const bool reaches = mem & (ml != 0u) & (in_frag <= off - 1u);  // offset 0, or in front of the fragment
-    if (sn_ballot(crosses | reaches)) return false;
-    const bool first = mem & (in_frag == 0u) & (ostart != 0u);
-    if (first) t->ip[ostart >> 16] = seg + uint32_t(lane);
-    found += uint32_t(__builtin_popcountll(sn_ballot(first)));
+    // (one vector compare per ballot, the lane masks combined on the scalar unit; a lane that
+    // is no member has len 0)
+    const uint64_t crosses = sn_ballot(in_frag + len > kSnBlock);
+    // offset 0, or in front of the fragment
+    const uint64_t reaches = sn_ballot((mem ? ml : 0u) != 0u) & sn_ballot(in_frag <= off - 1u);
+    if (crosses | reaches) return false;
+    const uint64_t Fm = sn_ballot(len != 0u) & sn_ballot(in_frag == 0u) & sn_ballot(ostart != 0u);
+    if (__builtin_amdgcn_inverse_ballot_w64(Fm)) t->ip[ostart >> 16] = seg + uint32_t(lane);
+    found += uint32_t(__builtin_popcountll(Fm));
     op = uni(op + T);
     if (a_last == n) break;
     ipn = a_last;
@@ -1243,8 +1288,9 @@ __global__ __launch_bounds__(64 * kSnDecWaves) void snappy_uncompress_kernel(
       d.map = map;
       d.din = uint32_t(src & 3u);
       d.rin = sn_make_rsrc(src - d.din, (d.din + nin + 3u) & ~3u);
-      d.rout = sn_make_rsrc(dst + uint64_t(k) * kSnBlock, flen);
+      sn_set_out(d, dst + uint64_t(k) * kSnBlock);
       d.pn = d.poc = d.plb = d.pfb = d.prb = 0;
+      d.plit = d.prk = false;
       const int r = sn_decode_elems(d, ipe, ipk, flen, map, lane);
       if (r != 0 && lane == 0) status[f] = r;
     } else if (k == 0) {

@@ -61,7 +61,7 @@ constexpr size_t kHcTab = size_t(4) << kHcHashLog;  // head / bucket start, u32
 constexpr int kHcOptNum = 1 << 12;           // LZ4_OPT_NUM, lz4hc.c:75
 constexpr int kHcTrailing = 3;               // TRAILING_LITERALS, lz4hc.c:1290
 constexpr size_t kHcOptBytes = size_t(kHcOptNum + 64) * 16;  // price table of the optimal parser
-// + chain, rank, sorted (u16), tr (u32), opt (16 B entries)
+// + chain (u16), sorted (u32), tr (u32), opt (16 B entries)
 constexpr size_t kHcScratch = kHcTab + 3 * 65536 * 2 + 65536 * 4 + kHcOptBytes;
 constexpr unsigned kHcGrid = 4096;  // 16 waves per CU (the kernel fits 20)
 
@@ -69,8 +69,10 @@ struct HcBlock {
   uintptr_t s;       // block bytes (global)
   uint32_t *head;    // build: pos | rank << 16 per hash; then bucket start
   uint16_t *chain;   // DELTANEXTU16 per position
-  uint16_t *rank;    // index of the position inside its hash bucket
-  uint16_t *sorted;  // positions ordered by (hash, position)
+  // positions ordered by (hash, position), each with a fingerprint of its 4 bytes: position |
+  // (their low 16 bits) << 16.  The candidates of one bucket lie side by side, so ruling
+  // them out by fingerprint reads one line where their source bytes are one line each.
+  uint32_t *sorted;
   uint32_t *tr;      // per position: its index in sorted | its rank << 16
   int4 *opt;         // LZ4HC_optimal_t[]: x price, y off, z mlen, w litlen (levels 10..12)
   int attempts;      // nbSearches
@@ -191,7 +193,6 @@ __device__ void hc_build(const HcBlock &b, int npos) {
     const bool valid = p < npos;
     const uint32_t h = valid ? hc_hash(w_next) : 0u;
     w_next = p + 64 < npos ? ld32u(b.s + p + 64) : 0u;
-    if (valid) b.tr[p] = h;  // the scatter below reads the hash back from here
     const uint64_t eq = same_value_lanes<kHcHashLog>(h, ballot(valid));
     const uint32_t hv = valid ? b.head[h] : kHcNone;
     const uint64_t eb = eq & below;
@@ -202,7 +203,7 @@ __device__ void hc_build(const HcBlock &b, int npos) {
     if (valid) {
       const int d = p - prev;  // LZ4HC_Insert (lz4hc.c:125-132)
       b.chain[p] = uint16_t(d > 65535 ? 65535 : d);
-      b.rank[p] = uint16_t(rk);
+      b.tr[p] = h | (rk << 16);  // the scatter below takes hash and rank from here
       if (!(eq & above)) b.head[h] = uint32_t(p) | (rk << 16);
     }
     __threadfence_block();
@@ -235,22 +236,23 @@ __device__ void hc_build(const HcBlock &b, int npos) {
   __threadfence_block();
   // scatter, four steps' loads issued before their stores
   for (int p0 = lane; p0 < npos; p0 += 256) {
-    uint32_t h[4], r[4], st[4];
+    uint32_t t[4], v[4], st[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int p = p0 + 64 * j;
-      h[j] = p < npos ? b.tr[p] : 0u;
-      r[j] = p < npos ? uint32_t(b.rank[p]) : 0u;
+      t[j] = p < npos ? b.tr[p] : 0u;
+      v[j] = ld32u_nb(b.s + min(p, npos - 1));
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) st[j] = b.head[h[j]];
+    for (int j = 0; j < 4; ++j) st[j] = b.head[t[j] & 0x7FFFu];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int p = p0 + 64 * j;
       if (p < npos) {
-        const uint32_t idx = st[j] + r[j];
-        b.sorted[idx] = uint16_t(p);
-        b.tr[p] = idx | (r[j] << 16);
+        const uint32_t r = t[j] >> 16;
+        const uint32_t idx = st[j] + r;
+        b.sorted[idx] = uint32_t(p) | (v[j] << 16);
+        b.tr[p] = idx | (r << 16);
       }
     }
   }
@@ -379,7 +381,7 @@ __device__ int hc_search_edge(const HcBlock &b, int ip, int ilow, int ihigh, int
   for (int c0 = 0; c0 < total; c0 += 64) {
     const int j = c0 + lane;
     const bool valid = j < total;
-    const int c = int(b.sorted[valid ? top - j : top]);
+    const int c = int(b.sorted[valid ? top - j : top] & 0xFFFFu);
     const bool ok32 = (ld32u_nb(s + c) == pat) & valid;  // (c < ip: inside the block as well)
     int back = 0, len = 0;
     if (ok32) {
@@ -467,12 +469,16 @@ __device__ int hc_search_w(const HcBlock &b, int ip, int ilow, int ihigh, int lo
     HC_CNT(4, 1);
     const int j = c0 + lane;
     const bool valid = j < total;
-    const int c = int(b.sorted[valid ? top - j : top]);
+    const uint32_t se = b.sorted[valid ? top - j : top];
+    // a candidate whose fingerprint differs cannot pass the MINMATCH test (lz4hc.c:266): its
+    // loads go to the position itself, lines the wave holds already
+    const bool fpok = valid & ((se >> 16) == (pat & 0xFFFFu));
+    const int c = fpok ? int(se & 0xFFFFu) : ip;
     uint32_t cw[9], cb[2];
-    hc_load_words<9>(s + c, cw);  // (c < ip)
+    hc_load_words<9>(s + c, cw);  // (c <= ip)
     const bool cback = wideback && c >= 8;
     hc_load_words<2>(s + (cback ? c - 8 : c), cb);
-    const bool ok32 = (cw[0] == pat) & valid;
+    const bool ok32 = (cw[0] == pat) & fpok;
     int fwd = 32;
 #pragma unroll
     for (int k = 8; k >= 1; --k) {
@@ -609,10 +615,12 @@ __device__ __forceinline__ int hc_encode(const HcBlock &b, uintptr_t d, int &op,
 // 4 bytes at p (the only way such a search can succeed; lz4hc.c:264-266).
 // Positions it cannot settle cheaply (long buckets, level-9 repetitive
 // patterns) report false and get the full search.
+constexpr int kHcSure = 8;  // candidates a position may have and still be settled here
 __device__ __forceinline__ bool hc_sure_miss(const HcBlock &b, int p, int mflimit) {
   // every load is unconditional on a clamped address (a predicated load is waited for at
-  // once): three dependent round trips per 64 positions, not one per candidate.  A
-  // position up to mflimit has 11 block bytes behind it, so the 8-byte reads stay inside.
+  // once): two dependent round trips per 64 positions (the position's table entry, then its
+  // candidates' fingerprints), not one per candidate.  A position up to mflimit has 11 block
+  // bytes behind it, so the 8-byte read stays inside.
   const bool in = p <= mflimit;
   const int pc = in ? p : mflimit;
   const uint32_t pat = ld32u_nb(b.s + pc);
@@ -622,19 +630,18 @@ __device__ __forceinline__ bool hc_sure_miss(const HcBlock &b, int p, int mflimi
   const int total = r < b.attempts ? r : b.attempts;
   const int top = int(t & 0xFFFFu) - 1;
   // positions that cannot be settled here read nothing of their own (their loads go to the
-  // position itself, a line the wave has already touched)
-  const bool open = !in || rep || total > 8;
+  // first fingerprint, one line for the wave)
+  const bool open = !in || rep || total > kHcSure;
   const int nt = open ? 0 : total;
-  int c[8];
+  // a candidate whose fingerprint differs from the position's cannot repeat its 4 bytes; one
+  // that matches it is left to the full search
+  uint32_t w[kHcSure];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) c[j] = int(b.sorted[j < nt ? top - j : 0]);
-  uint32_t w[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) w[j] = ld32u_nb(b.s + (j < nt ? c[j] : pc));
+  for (int j = 0; j < kHcSure; ++j) w[j] = b.sorted[j < nt ? top - j : 0] >> 16;
   bool miss = true;
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    if (j < nt && w[j] == pat) miss = false;
+  for (int j = 0; j < kHcSure; ++j)
+    if (j < nt && w[j] == (pat & 0xFFFFu)) miss = false;
   return !open && miss;  // (total == 0: nothing to test)
 }
 
@@ -780,7 +787,7 @@ __device__ int hc_search_swap(const HcBlock &b, int ip, int ihigh, int longest, 
     for (int c0 = 0; c0 < total; c0 += 64) {
       const int j = c0 + lane;
       const bool inq = j < total;
-      const int m = int(b.sorted[inq ? top - j : top]) - cp;  // (clamped, not predicated)
+      const int m = int(b.sorted[inq ? top - j : top] & 0xFFFFu) - cp;  // (clamped, not predicated)
       const bool valid = inq && m >= 0;
       bool ok32;
       int len = 0;
@@ -1076,8 +1083,8 @@ __global__ __launch_bounds__(kHcBuildThreads) void lz4hc_build_kernel(
     const uintptr_t s = reinterpret_cast<uintptr_t>(in) + in_offs[f] + uint64_t(k) * kLz4Block;
     uint8_t *sc = scratch + size_t(it - it0) * kHcScratch;
     uint16_t *chain = reinterpret_cast<uint16_t *>(sc + kHcTab);
-    uint16_t *sorted = chain + 2 * 65536;
-    uint32_t *tr = reinterpret_cast<uint32_t *>(sorted + 65536);
+    uint32_t *sorted = reinterpret_cast<uint32_t *>(chain + 65536);
+    uint32_t *tr = sorted + 65536;
     for (int i = tid; i < (1 << kHcHashLog); i += kHcBuildThreads) head[i] = kHcNone;
     __syncthreads();
     if (wave == 0) {
@@ -1151,11 +1158,15 @@ __global__ __launch_bounds__(kHcBuildThreads) void lz4hc_build_kernel(
     __syncthreads();
     // scatter, four steps' loads issued before their stores
     for (int p0 = tid; p0 < npos; p0 += 4 * kHcBuildThreads) {
-      uint32_t t[4];
+      uint32_t t[4], v0[4], v1[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int p = p0 + kHcBuildThreads * j;
         t[j] = p < npos ? tr[p] : 0u;
+        // the position's 4 bytes for its fingerprint (clamped, not predicated)
+        const uintptr_t a = (s + min(p, npos - 1)) & ~uintptr_t(3);
+        v0[j] = *(g_cu32 *)a;
+        v1[j] = *(g_cu32 *)(a + 4);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1163,7 +1174,8 @@ __global__ __launch_bounds__(kHcBuildThreads) void lz4hc_build_kernel(
         if (p < npos) {
           const uint32_t r = t[j] >> 16;
           const uint32_t idx = head[t[j] & 0x7FFFu] + r;
-          sorted[idx] = uint16_t(p);
+          sorted[idx] = uint32_t(p) |
+                        (__builtin_amdgcn_alignbyte(v1[j], v0[j], uint32_t((s + p) & 3u)) << 16);
           tr[p] = idx | (r << 16);
         }
       }
@@ -1204,9 +1216,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     uint8_t *sc = scratch + size_t(it - it0) * kHcScratch;
     b.head = reinterpret_cast<uint32_t *>(sc);
     b.chain = reinterpret_cast<uint16_t *>(sc + kHcTab);
-    b.rank = b.chain + 65536;
-    b.sorted = b.rank + 65536;
-    b.tr = reinterpret_cast<uint32_t *>(b.sorted + 65536);
+    b.sorted = reinterpret_cast<uint32_t *>(b.chain + 65536);
+    b.tr = b.sorted + 65536;
     b.opt = reinterpret_cast<int4 *>(b.tr + 65536);
     const uint32_t f = it % n, kk = it / n;
     const uint32_t len = uni(in_lens[f]);

@@ -55,23 +55,47 @@ __device__ __forceinline__ void crcw_load_t0(crcw_lds_u32 *t0, const uint32_t *_
 }
 
 // Raw CRC32C register (zero in, no inversion) of the `len` bytes at `addr`, whole wave;
-// the result is wave-uniform.  Lane l takes the l-th piece of P = ceil(len/64) bytes
-// counted from the END of the range (the front lanes' missing bytes are leading zeros),
-// byte by byte through T0; the 64 registers combine in a shift-and-xor scan.
+// the result is wave-uniform.  Lane l takes piece l of P = ceil(len/64) bytes counted from
+// the start (q full pieces, one of `rem` bytes, the rest empty), byte by byte through T0.
+// The bytes come as aligned dwords through a range-checked resource (reads past the end
+// return 0), 16 per step on unconditional loads, the next step's issued before this step's
+// table chain -- a load under a lane predicate would be waited for at once, one memory
+// round trip per byte.  The full pieces' registers combine in a shift-and-xor scan; the
+// short piece follows behind a shift by its length.
 __device__ __forceinline__ uint32_t wave_crc_raw(uintptr_t addr, uint32_t len,
                                                  const crcw_lds_u32 *t0,
                                                  const uint32_t *__restrict__ x2n, int lane) {
   if (!len) return 0u;
   const uint32_t P = (len + 63u) / 64u;
-  const int64_t hi = int64_t(len) - int64_t(63 - lane) * int64_t(P);  // piece = [hi - P, hi)
-  const int64_t lo = hi - int64_t(P);
+  const uint32_t q = len / P, rem = len - q * P;  // 1 <= q <= 64
+  const uint32_t start = uint32_t(lane) * P;
+  const uint32_t mine = start >= len ? 0u : (len - start < P ? len - start : P);
+  const uint32_t sa = uint32_t(addr & 3u);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void *>(addr - sa), 0, int((sa + len + 3u) & ~3u), 0x00020000);
+  typedef uint32_t crcw_u4 __attribute__((ext_vector_type(4)));
+  const uint32_t v0 = start + sa, sh = v0 & 3u;
   uint32_t r = 0;
-  for (uint32_t k = 0; k < P; ++k) {
-    const int64_t at = lo + int64_t(k);
-    const uint32_t b = at >= 0 ? ldb(addr + uint64_t(at)) : 0u;
-    r = t0[(r ^ b) & 0xFFu] ^ (r >> 8);
+  crcw_u4 na = __builtin_amdgcn_raw_buffer_load_b128(rs, v0 & ~3u, 0, 0);
+  uint32_t nb = __builtin_amdgcn_raw_buffer_load_b32(rs, (v0 & ~3u) + 16u, 0, 0);
+  for (uint32_t k = 0; k < P; k += 16u) {
+    const crcw_u4 a = na;
+    const uint32_t e = nb;
+    na = __builtin_amdgcn_raw_buffer_load_b128(rs, ((v0 + k) & ~3u) + 16u, 0, 0);
+    nb = __builtin_amdgcn_raw_buffer_load_b32(rs, ((v0 + k) & ~3u) + 32u, 0, 0);
+    const uint32_t w[4] = {__builtin_amdgcn_alignbyte(a.y, a.x, sh), __builtin_amdgcn_alignbyte(a.z, a.y, sh),
+                           __builtin_amdgcn_alignbyte(a.w, a.z, sh), __builtin_amdgcn_alignbyte(e, a.w, sh)};
+#pragma unroll
+    for (uint32_t j = 0; j < 16u; ++j) {
+      const uint32_t byte = (w[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
+      const uint32_t nr = t0[(r ^ byte) & 0xFFu] ^ (r >> 8);
+      r = k + j < mine ? nr : r;
+    }
   }
+  // S(L) = sum over l <= L of r_l * X^(L-l), X = x^(8P): the full pieces, at lane q-1
   uint32_t X = uint32_t(__builtin_amdgcn_readfirstlane(int(crcw_xpow8n(P, x2n))));  // x^(8P)
+  const uint32_t r_short = uint32_t(__builtin_amdgcn_readlane(int(r), int(q & 63u)));  // (rem == 0: unused)
+  if (uint32_t(lane) >= q) r = 0;
 #pragma unroll 1
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t t = uint32_t(__shfl_up(int(r), d));
@@ -79,7 +103,8 @@ __device__ __forceinline__ uint32_t wave_crc_raw(uintptr_t addr, uint32_t len,
     if (lane >= d) r ^= m;
     X = crcw_mul(X, X);
   }
-  return uint32_t(__builtin_amdgcn_readlane(int(r), 63));
+  const uint32_t full = uint32_t(__builtin_amdgcn_readlane(int(r), int(q - 1u)));
+  return rem ? crcw_shift(full, rem, x2n) ^ r_short : full;
 }
 
 }  // namespace rdk

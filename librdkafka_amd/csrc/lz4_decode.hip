@@ -80,19 +80,34 @@ __device__ __forceinline__ uint32_t win_byte(InWin &w, uintptr_t p, int lane) {
 // ---------------------------------------------------------- byte movers
 __device__ __forceinline__ void copy_fwd(uintptr_t d, uintptr_t s, uint32_t len, int lane) {
   asm volatile("" ::: "memory");
-  for (uint32_t base = 0; base < len; base += 256u) {
-    uint32_t v[4];
+  // up to 3 bytes bring the destination to a dword boundary; then a dword per lane and step
+  // (four steps' loads in flight), each made of the two aligned source dwords it lies in,
+  // read through a range-checked resource (nothing is touched past the source's end); the
+  // last 0..3 bytes by lanes again
+  uint32_t head = uint32_t((4u - uint32_t(d & 3u)) & 3u);
+  head = head < len ? head : len;
+  if (uint32_t(lane) < head) stb(d + uint32_t(lane), ldb(s + uint32_t(lane)));
+  const uintptr_t d4 = d + head, s4 = s + head;
+  const uint32_t n4 = (len - head) >> 2;
+  const uint32_t sh = uint32_t(s4 & 3u);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void *>(s4 - sh), 0, int((sh + (len - head) + 3u) & ~3u), 0x00020000);
+  for (uint32_t base = 0; base < n4; base += 256u) {
+    uint32_t lo[4], hi[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t i = base + lane + 64u * j;
-      v[j] = i < len ? ldb(s + i) : 0u;
+      const uint32_t i = base + uint32_t(lane) + 64u * uint32_t(j);
+      lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, 4u * i, 0, 0);  // (past the end: 0)
+      hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, 4u * i + 4u, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t i = base + lane + 64u * j;
-      if (i < len) stb(d + i, v[j]);
+      const uint32_t i = base + uint32_t(lane) + 64u * uint32_t(j);
+      if (i < n4) *(g_u32 *)(d4 + 4u * i) = __builtin_amdgcn_alignbyte(hi[j], lo[j], sh);
     }
   }
+  const uint32_t done = head + 4u * n4;
+  if (uint32_t(lane) < len - done) stb(d + done + uint32_t(lane), ldb(s + done + uint32_t(lane)));
   asm volatile("" ::: "memory");
 }
 

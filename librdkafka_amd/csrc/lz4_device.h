@@ -10,6 +10,7 @@ namespace rdk {
 typedef __attribute__((address_space(1))) const uint8_t g_cu8;
 typedef __attribute__((address_space(1))) uint8_t g_u8;
 typedef __attribute__((address_space(1))) const uint32_t g_cu32;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
 
 constexpr int kLz4MinMatch = 4;
 constexpr int kLz4LastLiterals = 5;   // lz4.c:192

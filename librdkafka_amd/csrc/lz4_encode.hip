@@ -117,7 +117,7 @@ __device__ __forceinline__ void wave_copy(uintptr_t d, uintptr_t s, uint32_t len
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t i = base + lane + 64u * j;
-      v[j] = i < len ? ldb(s + i) : 0u;
+      v[j] = ldb(s + (i < len ? i : len - 1u));  // (clamped, not predicated)
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -91,8 +91,10 @@ __device__ __forceinline__ void wave_copy_bytes(uintptr_t d, uintptr_t s, uint32
     uint32_t v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      // (clamped, not predicated: a load under a lane predicate is waited for at once, and
+      // the four would be four round trips)
       const uint32_t i = base + lane + 64u * j;
-      v[j] = i < len ? ldb(s + i) : 0u;
+      v[j] = ldb(s + (i < len ? i : len - 1u));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -161,8 +161,8 @@ __device__ __forceinline__ void hc_copy(uintptr_t d, uintptr_t s, int len, int l
     uint32_t v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int i = base + lane + 64 * j;
-      v[j] = i < len ? ldb(s + i) : 0u;
+      const int i = base + lane + 64 * j;  // (clamped, not predicated: see wave_copy_bytes)
+      v[j] = ldb(s + (i < len ? i : len - 1));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -286,14 +286,18 @@ __device__ __forceinline__ bool generic_search(uintptr_t src, int mflimitPlusOne
     const int Pn = fwd + int(incl);
     const bool valid = Pn <= mflimitPlusOne;
     const uint64_t vmask = ballot(valid);
-    const uint32_t seq = valid ? ld32u(src + uint32_t(P)) : 0u;
+    // (a valid probe and every table entry have 12 block bytes behind them: the branch-free
+    // 8-byte reads stay inside; a load under a lane predicate would be waited for at once)
+    const uint32_t sv = ld32u_nb(src + uint32_t(valid ? P : 0));
+    const uint32_t seq = valid ? sv : 0u;
     const uint32_t h = lz4_hash(seq);
     uint64_t eq = same_value_lanes<int(kHashLog)>(h, vmask);
     const uint64_t lower = eq & ((1ull << lane) - 1ull);
     const int pred = lower ? 63 - __builtin_clzll(lower) : 0;
     const int predP = __shfl(P, pred);
     const int cand = lower ? predP : int(table[h]);
-    const bool m = valid && ld32u(src + uint32_t(cand)) == seq;
+    const uint32_t cv = ld32u_nb(src + uint32_t(valid ? cand : 0));
+    const bool m = valid && cv == seq;
     const uint64_t mm = ballot(m);
     const int f = ffs64(mm);
     const int e = ffs64(~vmask);

@@ -278,14 +278,19 @@ __device__ __forceinline__ bool sn_generic_search(const SnFrag &b, uint32_t fwd,
     const uint32_t P = fwd + incl - s, Pn = fwd + incl;
     const bool valid = int(Pn) <= b.ip_limit;
     const uint64_t vmask = ballot(valid);
-    const uint32_t seq = valid ? ld32u(b.src + P) : 0u;
+    // (a valid probe and every table entry have 15 fragment bytes behind them: the
+    // branch-free 8-byte reads stay inside; a load under a lane predicate would be waited
+    // for at once)
+    const uint32_t sv = ld32u_nb(b.src + (valid ? P : 0u));
+    const uint32_t seq = valid ? sv : 0u;
     const uint32_t h = (seq * kSnMul) >> b.shift;
     uint64_t eq = same_value_lanes<14>(h, vmask);
     const uint64_t lower = eq & ((1ull << lane) - 1ull);
     const int pred = lower ? 63 - __builtin_clzll(lower) : 0;
     const uint32_t predP = uint32_t(__shfl(int(P), pred));
     const uint32_t cd = lower ? predP : uint32_t(table[h]);
-    const bool m = valid && ld32u(b.src + cd) == seq;
+    const uint32_t cv = ld32u_nb(b.src + (valid ? cd : 0u));
+    const bool m = valid && cv == seq;
     const uint64_t mm = ballot(m);
     const int f = ffs64(mm);
     const int e = ffs64(~vmask);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- librdkafka record-batch engine on MI355X.
 
-Headline = BASELINE.json's metric itself, "record-batch GB/s (CRC32C+LZ4F)": the writer's
+Headline = the metric "record-batch GB/s (CRC32C+LZ4F)": the writer's
 finalize of device-resident MsgVersion 2 MessageSets (rd_kafka_msgset_writer_finalize,
 rdkafka_msgset_writer.c:1335: LZ4F compress :1128-1221 with frames byte-identical to
 rd_kafka_lz4_compress, header finalize :1251-1295, CRC32C :1229-1246) over `--partitions`
@@ -74,7 +74,7 @@ def profile_summary(leg: str, alg_bytes: int, kernel_ms: float):
 
 
 def shard_partitions(n_partitions: int, rank: int, world: int) -> list[int]:
-    """toppar -> GPU round-robin (SURVEY §8e): partition p runs on rank p % world."""
+    """toppar -> GPU round-robin: partition p runs on rank p % world."""
     return [p for p in range(n_partitions) if p % world == rank]
 
 
@@ -457,7 +457,7 @@ def tiled_messages(n_batches, per_batch, seed=42):
 
 
 def bench_serialize(args, rank, world, n=None, per_batch=9500):
-    """SURVEY §8f rank 1 / configs[4] shape: linger-accumulated ~1 MiB MsgVersion 2
+    """The record writer (rdkafka_msgset_writer.c:652-754), configs[4] shape: linger-accumulated ~1 MiB MsgVersion 2
     batches of ~100-byte JSON records built on the device (record sizes + scan, record
     writer, CRC32C finalize) from per-message key / value / header arrays."""
     import ctypes as C
@@ -498,7 +498,7 @@ def bench_serialize(args, rank, world, n=None, per_batch=9500):
 
 
 def bench_index(args, rank, world, n=None, per_batch=9500):
-    """the consumer's record index (rd_kafka_msgset_reader_msg_v2,
+    """The consumer's record index (rd_kafka_msgset_reader_msg_v2,
     rdkafka_msgset_reader.c:715-927) over ~1 MiB MsgVersion 2 batches of ~100-byte JSON
     records (built on the device by the record writer): one row per record with offset,
     timestamp, key / value / headers positions."""
@@ -623,7 +623,7 @@ def bench_chain(args, rank, world, n=None, per_batch=9500):
 
 
 def bench_legacy(args, rank, world, n=None, set_bytes=1 << 20):
-    """SURVEY §8f rank 4: MsgVersion 1 MessageSets (~1 MiB of ~150-byte JSON messages each)
+    """MsgVersion 1 MessageSets (~1 MiB of ~150-byte JSON messages each)
     through the consumer's per-message check.crcs (rd_kafka_msgset_reader_msg_v0_1,
     rdkafka_msgset_reader.c:566-628: message walk + CRC-32 of [16, 12+MessageSize)).
     The sets are laid out on the host, tiled, and given their CRCs by the engine's FINALIZE

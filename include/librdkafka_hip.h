@@ -8,7 +8,7 @@
  *  1. DROP-IN symbols.  Exactly the internal librdkafka v1.3.0 functions the
  *     MessageSet writer/reader call through the PLT, with identical
  *     signatures, ownership and error contracts.  Preloading (or linking
- *     ahead of librdkafka.so) interposes them; see INTEGRATION.md.
+ *     ahead of librdkafka.so) interposes them.
  *
  *  2. ENGINE batch API (rdk_hip_*).  Device-resident batches of many
  *     toppars' record batches, processed in one launch per stage on a caller
@@ -272,7 +272,7 @@ int rdk_hip_lz4f_decompress_noalloc(const void *d_in, const uint64_t *d_in_offs,
                                     void *stream);
 
 /* ---------------------------------------------------------------------------
- * Producer batching front-end (north_star).  One
+ * Producer batching front-end (pinned staging rings, copies overlapped with kernels).  One
  * producer per broker thread: a ring of `nslots` pinned host staging slots,
  * each with its own device buffers and HIP stream.  produce() gathers one
  * MsgVersion 2 batch -- the 61-byte header as the writer leaves it
@@ -326,7 +326,7 @@ int rdk_hip_producer_flush(rdk_hip_producer_t *p);
 int rdk_hip_producer_poll(rdk_hip_producer_t *p, rdk_hip_batch_t *out, int max, int block);
 void rdk_hip_producer_destroy(rdk_hip_producer_t *p);
 
-/* ---- MsgVersion 2 record serialisation --------------------
+/* ---- MsgVersion 2 record serialisation ---------------------------------------
  * For device-resident messages, replaces
  *   rd_kafka_msgset_writer_write_MessageSet_v2_header  rdkafka_msgset_writer.c:352-403
  *   rd_kafka_msgset_writer_write_msg_v2                 rdkafka_msgset_writer.c:652-754
@@ -366,7 +366,7 @@ int rdk_hip_msgset_v2_write(const rdk_hip_msgs_t *msgs, const rdk_hip_v2_batch_t
                             const uint64_t *d_out_offs, uint8_t *d_out, uint32_t *d_crc,
                             void *stream);
 
-/* ---- MsgVersion 2 record index ------------------------------
+/* ---- MsgVersion 2 record index -------------------------------------------------
  * rd_kafka_msgset_reader_msg_v2 (rdkafka_msgset_reader.c:715-927) for every record of
  * n batches, on the device: batch i's header (BaseOffset, BaseTimestamp) at
  * d_hdr_base + d_hdr_offs[i], its (uncompressed / decompressed) records at
@@ -402,7 +402,7 @@ int rdk_hip_msgset_v2_index(const void *d_hdr_base, const uint64_t *d_hdr_offs,
 int rdk_hip_gen_v2_batches(void *d_base, uint32_t n, uint32_t batch_size,
                            uint64_t seed, void *stream);
 
-/* Host-side JSON-like record stream (DESIGN.md "Workloads"): exactly `len`
+/* Host-side JSON-like record stream: exactly `len`
  * bytes of `{"id":..,"user":"u.....","ts":..,"event":"..","value":..}\n`
  * records from the LCG s = s*1103515245+12345 seeded with `seed`. */
 void rdk_hip_gen_json(uint8_t *dst, size_t len, uint32_t seed);

@@ -4,7 +4,7 @@
 // as called by the MessageSet writer (rdkafka_msgset_writer.c:1229-1246) and
 // reader (rdkafka_msgset_reader.c:982-1015).
 //
-// Design (DESIGN.md "CRC32C"):
+// Design:
 //   * one wavefront per byte range (a record batch), persistent grid;
 //   * lane l of iteration k owns the 16-byte vector at V + 1024k + 16l, so
 //     every global_load_dwordx4 of the wave reads 1 KiB contiguous (coalesced);

@@ -1,4 +1,4 @@
-// legacy.hip -- MsgVersion 0/1 MessageSets: the per-message CRC-32 (SURVEY §8f rank 4).
+// legacy.hip -- MsgVersion 0/1 MessageSets: the per-message CRC-32.
 //
 // Reference (bluelichen19/librdkafka v1.3.0):
 //   writer  rd_kafka_msgset_writer_write_msg_v0_1  src/rdkafka_msgset_writer.c:583-645
@@ -35,7 +35,7 @@ struct V01 {
     if (R < 16u) return kPartial;                     // Offset, MessageSize, Crc :566-570
     if (p + 16u > W.end) return kCut;
     const int32_t s = int32_t(W.be32(p + 8u));
-    if (s < 4) return kErr;                           // see DESIGN: the reference asserts
+    if (s < 4) return kErr;  // (MessageSize - 4 wraps: rd_slice_narrow_copy asserts, rdbuf.c:1027)
     if (uint32_t(s) - 4u > R - 16u) return kPartial;  // narrow_copy / check_len :571-573
     if (R < 18u) return kPartial;                     // MagicByte, Attributes :575-576
     if (p + 18u > W.end) return kCut;

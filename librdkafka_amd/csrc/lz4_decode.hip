@@ -4,7 +4,7 @@
 // LZ4F_decompress (lz4frame.c:1371) -> LZ4_decompress_safe_usingDict
 // (lz4.c:2307 -> LZ4_decompress_generic lz4.c:1654-2068).
 //
-// Pipeline per batch of frames (DESIGN.md "LZ4F decode"):
+// Pipeline per batch of frames:
 //   1. walk kernel   : one lane per frame parses the header and block table
 //                      (FrameWalker, lz4_frame.h) into descriptors;
 //   2. block kernel  : one wavefront per independent block decodes straight

@@ -1,4 +1,4 @@
-// records.hip -- MsgVersion 2 record serialisation on gfx950.
+// records.hip -- MsgVersion 2 record serialisation and record index on gfx950.
 //
 // Replaces, for device-resident messages:
 //   rd_kafka_msgset_writer_write_MessageSet_v2_header  rdkafka_msgset_writer.c:352-403
@@ -8,7 +8,7 @@
 // with the batch loop semantics of write_msgq (:804-902): OffsetDelta = index in
 // the batch, TimestampDelta against the first message, MaxTimestamp from 0.
 //
-// Record index (rdkafka_msgset_reader.c:715-927, SURVEY §8f rank 2): see v2_index_kernel.
+// Record index (rdkafka_msgset_reader.c:715-927): see v2_index_kernel.
 //
 // Workgroups of 256 threads work on chunks of 256 records (grid = chunks x batches):
 //   sizes: a thread sizes one record (zig-zag varints, rdvarint.h:48-75), a chunk scan
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch
   }
 }
 
-// ---- record index (SURVEY §8f rank 2): rd_kafka_msgset_reader_msg_v2
+// ---- record index: rd_kafka_msgset_reader_msg_v2
 // (rdkafka_msgset_reader.c:715-927) for every record of a batch, one row each.
 // One wavefront per batch.  The records are staged through an 8 KiB LDS window (16-byte
 // buffer loads): lane 0 walks the Length chain (:736-737) over it -- one LDS round trip

@@ -73,7 +73,7 @@ RDK_API int rdk_hip_gen_v2_batches(void *d_base, uint32_t n, uint32_t batch_size
   return RDK_HIP_OK;
 }
 
-// JSON-like record stream (DESIGN.md "Workloads"); byte-identical to
+// JSON-like record stream; byte-identical to
 // librdkafka_amd.workload.gen_json().
 RDK_API void rdk_hip_gen_json(uint8_t *dst, size_t len, uint32_t seed) {
   static const char *const kEvents[4] = {"click", "view", "purchase", "scroll"};

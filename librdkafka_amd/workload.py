@@ -1,10 +1,10 @@
-"""Deterministic synthetic workloads (DESIGN.md "Workloads").
+"""Deterministic synthetic workloads.
 
-* JSON-like record stream (BASELINE configs 3-5): records
+* JSON-like record stream (the compress / decompress / producer configurations): records
   ``{"id":N,"user":"uUUUUU","ts":T,"event":"E","value":V.FF}\\n`` drawn from
   the LCG ``s = s*1103515245 + 12345 (mod 2^32)``, each draw using ``s >> 8``;
   seed 42.  Byte-identical to the native ``rdk_hip_gen_json``.
-* MsgVersion 2 record batches (BASELINE config 2): 61-byte big-endian v2
+* MsgVersion 2 record batches (the CRC32C-only configuration): 61-byte big-endian v2
   header (rdkafka_msgset_writer.c:352-403) + splitmix64 bytes; every 8-byte
   word w of the buffer is ``splitmix64(seed + w)`` (seed 0x5EED), identical
   to the device generator ``rdk_hip_gen_v2_batches``.

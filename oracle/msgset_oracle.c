@@ -1,6 +1,6 @@
 /*
  * msgset_oracle.c -- CPU restatement of the MsgVersion 2 record writer and
- * record parser (SURVEY §8f ranks 1 and 2).  TEST INFRASTRUCTURE ONLY.
+ * record parser.  TEST INFRASTRUCTURE ONLY.
  *
  * Reference (bluelichen19/librdkafka v1.3.0):
  *   varints     src/rdvarint.h:48-75 (encode), :114-141 (decode)
@@ -13,7 +13,7 @@
  *   parser      src/rdkafka_msgset_reader.c:715-927 (reader_msg_v2)
  *
  * Parity pinning: rdvarint.h includes rd.h, which needs the generated config.h,
- * so the reference cannot be compiled here (DESIGN.md "Oracle").  The varint
+ * so the reference cannot be compiled here.  The varint
  * codec is pinned by the reference's own known answers (rdvarint.c:
  * unittest_rdvarint, tests/golden/varint_kat.json); the record layout is a
  * field-by-field restatement of the lines above ("parity unpinned" beyond the
@@ -164,7 +164,7 @@ long or_msgset_v2_index(const uint8_t *rec, size_t len, int64_t base_offset, int
 }
 
 /* ======================================================================
- * MsgVersion 0/1.
+ * MsgVersion 0/1 MessageSets and their per-message CRC-32.
  *
  *   CRC-32     rdcrc32.h:93-131; the reference is configured WITH_ZLIB, so this is zlib's
  *              crc32() (reflected 0xedb88320, ~0 in and out, chainable).  Restated here as

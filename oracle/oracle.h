@@ -9,7 +9,7 @@
  * Each function cites the reference file:line it restates
  * (reference = bluelichen19/librdkafka v1.3.0 with its vendored lz4 1.9.2).
  *
- * Parity pinning (see DESIGN.md "Oracle"):
+ * Parity pinning:
  *   - CRC32C: crc32c.c depends on the generated ../config.h (rd.h:64) and is
  *     therefore unbuildable here; the restatement is pinned by the reference's
  *     own known-answer test (crc32c.c:388-438, 0x7dcde113), the standard check
@@ -110,7 +110,7 @@ int or_lz4f_decompress_batches_mt(const uint8_t *base, const uint64_t *offs,
                                   int threads);
 
 
-/* ---- MsgVersion 2 records (msgset_oracle.c) ---------- */
+/* ---- MsgVersion 2 records: writer and parser (msgset_oracle.c) -------------- */
 /* rdvarint.h:48-75 / :114-141 (zig-zag varints) */
 size_t   or_varint_enc_i64(uint8_t *dst, int64_t num);
 size_t   or_varint_dec_i64(const uint8_t *src, size_t srcsize, int64_t *nump);

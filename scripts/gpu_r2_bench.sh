@@ -1,4 +1,4 @@
-# Round-2: producer/finalize tests, then the default bench line.
+# Producer/finalize tests, then the default bench line.
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R"
 O="$R/gpurun_out/r2bench"; mkdir -p "$O"

@@ -1,4 +1,4 @@
-# Round-2 GPU check: parity suite (+ the not yet collected no-alloc test), smoke, short bench.
+# GPU check: parity suite (+ the not yet collected no-alloc test), smoke, short bench.
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R"
 O="$R/gpurun_out/r2check"; mkdir -p "$O"

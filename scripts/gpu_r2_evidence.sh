@@ -1,4 +1,4 @@
-# Round-2 evidence: per-leg rocprofv3 summaries (trace + HBM counters), instruction-mix
+# Evidence for the current build: per-leg rocprofv3 summaries (trace + HBM counters), instruction-mix
 # counters of the exact compressor and the decoder, then the default bench line.
 # Copy gpurun_out/prof_r2/summaries/*, gpurun_out/r2lz4c_pmc/table.txt,
 # gpurun_out/r2dec_pmc/table.txt and gpurun_out/r2bench/bench.json into profiles/r02/.

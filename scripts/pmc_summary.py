@@ -6,7 +6,7 @@ Layout expected (as written by scripts/profile_*.sh):
   <dir>/pmc_write/*_counter_collection.csv (--pmc WRITE_SIZE)
   <dir>/pmc_sq/*_counter_collection.csv    (--pmc SQ_* group, optional)
 
-HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+HBM traffic per launch, counted as the MI355X microarchitecture guide prescribes: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
 (16 B/lane) streaming read, so it is doubled.  bench.py reads `traffic_bytes`
 from the summary of the kernel and workload it measures.

@@ -3,12 +3,12 @@
  * librdkafka.so as far as symbol binding goes.  The internal functions of the hot path
  * (crc32c, rd_slice_crc32c, rd_kafka_lz4_compress, rd_kafka_lz4_decompress) are defined
  * here with default visibility and reached by their callers through the PLT, exactly as
- * SURVEY's objdump of the reference build shows (`call crc32c@plt` from rd_slice_crc32c,
+ * an objdump of the reference's CMake build shows (`call crc32c@plt` from rd_slice_crc32c,
  * `call rd_slice_crc32c@plt` from the writer, ...).  The definitions here are deliberately
  * NOT the reference's code: crc32c is a bit-at-a-time loop and the LZ4 functions only
  * report that they ran.  The test preloads librdkafka_hip.so and checks that the CALLERS
  * in this library then reach the engine's definitions instead (ELF symbol interposition),
- * which is the binding INTEGRATION.md describes for the real library.
+ * which is how the engine binds to the real library under LD_PRELOAD.
  *
  * Build: gcc -O1 -fPIC -shared -o libhostpath.so hostlib.c
  */

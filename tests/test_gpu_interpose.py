@@ -1,4 +1,4 @@
-"""The binding INTEGRATION.md describes, exercised end to end: a program linked only
+"""The preload binding, exercised end to end: a program linked only
 against a host library that defines crc32c / rd_slice_crc32c / rd_kafka_lz4_compress /
 rd_kafka_lz4_decompress itself (default visibility, called through the PLT, like the
 reference's CMake build) is run twice -- plainly, and with librdkafka_hip.so preloaded.

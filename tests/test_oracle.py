@@ -80,7 +80,7 @@ def test_lz4f_decode_cases_match_reference_golden(oracle_mod, golden):
 
 def test_header_bytes_constant(oracle_mod):
     err, fr = oracle_mod.rdk_lz4_compress(b"x" * 100)
-    assert fr[:7] == bytes.fromhex("04224d18604082")
+    assert fr[:7] == bytes.fromhex("04224d18604082")       # LZ4F magic, FLG 0x60, BD 0x40, HC 0x82 (lz4frame.c:672-700)
     assert fr[-4:] == b"\x00\x00\x00\x00"
 
 

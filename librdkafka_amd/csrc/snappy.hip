@@ -946,16 +946,22 @@ __device__ __forceinline__ SnCand sn_parse_words(const SnDec &d, sn_u2 h, uint32
                                                  int lane) {
   const uint32_t p = seg + uint32_t(lane);
   const uint32_t w = __builtin_amdgcn_alignbyte(h.y, h.x, (p + d.din) & 3u);
+  // (flat selects over values already computed: nested ones compile to divergent branches)
   const uint32_t c = w & 0xFFu, kind = c & 3u, hi = c >> 2;
-  const uint32_t b1 = (w >> 8) & 0xFFu, b12 = (w >> 8) & 0xFFFFu, b123 = w >> 8;
+  const uint32_t b1 = (w >> 8) & 0xFFu, b12 = (w >> 8) & 0xFFFFu;
   const bool islit = kind == 0u;
-  const uint32_t lext = hi >= 60u ? hi - 59u : 0u;  // extra length bytes of a literal
-  const uint32_t k = 1u + (islit ? lext : kind == 1u ? 1u : kind == 2u ? 2u : 4u);
-  const bool complex = (islit & (lext == 4u)) | (kind == 3u);
-  const uint32_t lv = lext == 0u ? hi : lext == 1u ? b1 : lext == 2u ? b12 : b123;
+  const uint32_t lx = max(hi, 59u) - 59u;
+  const uint32_t lext = islit ? lx : 0u;  // extra length bytes of a literal
+  const uint32_t k = ((0x5321u >> (kind << 2)) & 15u) + lext;  // header bytes: 1+lext, 2, 3, 5
+  const bool complex = (lext == 4u) | (kind == 3u);
+  const uint32_t lvx = __builtin_amdgcn_ubfe(w, 8u, lext << 3);  // the lext bytes after the tag
+  const uint32_t lv = lext == 0u ? hi : lvx;
   const uint32_t ll = islit ? lv + 1u : 0u;
-  const uint32_t ml = islit ? 0u : kind == 1u ? 4u + (hi & 7u) : hi + 1u;
-  const uint32_t off = kind == 1u ? ((c >> 5) << 8) | b1 : b12;
+  const uint32_t m1 = 4u + (hi & 7u), m2 = hi + 1u;
+  const uint32_t mlc = kind == 1u ? m1 : m2;
+  const uint32_t ml = islit ? 0u : mlc;
+  const uint32_t o1 = ((c >> 5) << 8) | b1;
+  const uint32_t off = kind == 1u ? o1 : b12;
   SnCand r;
   const bool bad = (p >= csize) | (p + k > csize);  // refill_tag cannot complete the header
   r.A = bad ? kSnBad : complex ? kSnComplex : p + k + ll;
@@ -1151,6 +1157,57 @@ struct SnSplit {
   uint32_t ip[kSnFragMax];  // input position of fragment k's first element (k >= 1)
 };
 
+constexpr uint32_t kSnPoison = 0x04000000u;  // a length no stream that splits can reach
+constexpr int kSnScanGroup = 4;              // segments whose lists are collapsed together
+
+// The elements of one 64-byte segment reached from lane x0, with output positions from `op`:
+// false when one of them keeps the stream from being split (it crosses a 64 KiB boundary of
+// the output, copies from before its fragment, or cannot be parsed); records the input
+// position of every element that starts a fragment.
+__device__ bool sn_scan_members(const SnCand &cur, uint32_t n, uint32_t seg, uint32_t x0, uint32_t op,
+                                SnSplit *t, uint32_t &found, int lane) {
+  const bool stop = (cur.A - seg >= 64u) | (cur.A == n);
+  uint32_t J = stop ? 256u : (cur.A - seg) << 2;  // successor as a permute address; 256: none
+  bool R = uint32_t(lane) == x0;
+#pragma unroll
+  for (int level = 0; level < 5; ++level) {
+    const bool send = R & (J < 256u);
+    const int tt = __builtin_amdgcn_ds_permute(int(send ? J : x0 << 2), 1);
+    R = R | (tt != 0);
+    const uint32_t jj = uint32_t(__builtin_amdgcn_ds_bpermute(int(J), int(J)));
+    J = J < 256u ? jj : 256u;
+  }
+  const bool mem = R;
+  const uint32_t ra = R ? cur.A : 0u;                // (a member's A is never 0)
+  if (sn_ballot(ra >= kSnBad)) return false;         // kSnBad or kSnComplex
+  const uint32_t ml = cur.mk & 0xFFu, off = cur.off;
+  const uint32_t len = mem ? cur.ll + ml : 0u;
+  uint32_t T;
+  const uint32_t ostart = op + sn_excl_sum(len, T);
+  const uint32_t in_frag = ostart & (kSnBlock - 1u);
+  // (one vector compare per ballot, the lane masks combined on the scalar unit; a lane that
+  // is no member has len 0)
+  const uint64_t crosses = sn_ballot(in_frag + len > kSnBlock);
+  // offset 0, or in front of the fragment
+  const uint64_t reaches = sn_ballot((mem ? ml : 0u) != 0u) & sn_ballot(in_frag <= off - 1u);
+  if (crosses | reaches) return false;
+  const uint64_t Fm = sn_ballot(len != 0u) & sn_ballot(in_frag == 0u) & sn_ballot(ostart != 0u);
+  if (__builtin_amdgcn_inverse_ballot_w64(Fm)) t->ip[ostart >> 16] = seg + uint32_t(lane);
+  found += uint32_t(__builtin_popcountll(Fm));
+  return true;
+}
+
+// Whether a stream can be decoded by fragments, and where each fragment's input starts
+// (every 64 KiB of output begins at an element boundary and no copy reaches across one:
+// what the block-by-block writer, snappy.c:1344, produces).
+//
+// One wavefront follows the stream's elements from segment to segment. A segment's step
+// (entry lane -> output bytes, exit position, largest copy offset on the way) does not
+// depend on where the stream enters it, so the elements of a segment are collapsed by
+// pointer doubling for every entry lane at once, kSnScanGroup segments side by side (their
+// shuffles overlap); the dependent part per segment is then a handful of lane reads. Only a
+// segment whose output touches a 64 KiB boundary, or holds an offset larger than the
+// distance to the fragment's start, has its elements looked at one by one.
 __device__ bool sn_scan_stream(uintptr_t src, uint32_t n, uint32_t cap, SnSplit *t, int lane) {
   if (n >= 0x80000000u) return false;
   SnDec d;
@@ -1170,65 +1227,75 @@ __device__ bool sn_scan_stream(uintptr_t src, uint32_t n, uint32_t cap, SnSplit 
   }
   const uint32_t nfrag = (ulen + kSnBlock - 1u) / kSnBlock;
   if (ulen > cap || nfrag < 2u || nfrag > kSnFragMax || ip0 == n) return false;
+  constexpr int G = kSnScanGroup;
   uint32_t op = 0, ipn = ip0, found = 0;
-  uint32_t seg = ipn & ~63u;
-  SnCand cur = sn_parse(d, n, seg, lane);
-  // this pass runs at one wave per SIMD with nothing to hide a load behind: the header
-  // bytes of the next four segments are in flight
-  sn_u2 pf[4];
+  uint32_t base = ipn & ~63u;
+  sn_u2 pf[G];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) pf[j] = sn_parse_load(d, seg + 64u * uint32_t(j + 1), lane);
-  for (;;) {
-    const uint32_t x0 = ipn - seg;
-    const bool stop = (cur.A - seg >= 64u) | (cur.A == n);
-    uint32_t J = stop ? 256u : (cur.A - seg) << 2;  // successor as a permute address; 256: none
-    bool R = uint32_t(lane) == x0;
+  for (int g = 0; g < G; ++g) pf[g] = sn_parse_load(d, base + 64u * uint32_t(g), lane);
+  for (bool more = true; more;) {
+    SnCand c[G];
+    uint32_t P4[G], W[G], MX[G], L[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint32_t seg = base + 64u * uint32_t(g);
+      c[g] = sn_parse_words(d, pf[g], n, seg, lane);
+      pf[g] = sn_parse_load(d, seg + 64u * uint32_t(G), lane);  // the next group's
+      const uint32_t ml = c[g].mk & 0xFFu;
+      const bool stop = (c[g].A - seg >= 64u) | (c[g].A == n);
+      const bool poison = (c[g].A >= kSnBad) | ((ml != 0u) & (c[g].off == 0u));
+      L[g] = poison ? kSnPoison : c[g].ll + ml;
+      // a list: successor (the last element of the segment points at itself), bytes up to
+      // the successor, largest copy offset from here on
+      P4[g] = (stop ? uint32_t(lane) : c[g].A - seg) << 2;
+      W[g] = stop ? 0u : L[g];
+      MX[g] = ml != 0u ? c[g].off : 0u;
+    }
+    // (an element takes at least two bytes: at most 32 to a segment)
 #pragma unroll
     for (int level = 0; level < 5; ++level) {
-      const bool send = R & (J < 256u);
-      const int tt = __builtin_amdgcn_ds_permute(int(send ? J : x0 << 2), 1);
-      R = R | (tt != 0);
-      const uint32_t jj = uint32_t(__builtin_amdgcn_ds_bpermute(int(J), int(J)));
-      J = J < 256u ? jj : 256u;
-    }
-    const bool mem = R;
-    const uint32_t ra = R ? cur.A : 0u;  // (a member's A is never 0)
-    const uint64_t M = sn_ballot(ra != 0u);
-    if (sn_ballot(ra >= kSnBad)) return false;  // kSnBad or kSnComplex
-    const uint32_t xl = uint32_t(63 - __builtin_clzll(M));
-    const uint32_t a_last = uni(__builtin_amdgcn_readlane(cur.A, xl));
-    if (a_last > n) return false;
-    const uint32_t ll = cur.ll, ml = cur.mk & 0xFFu, off = cur.off;
-    const uint32_t len = mem ? ll + ml : 0u;
-    uint32_t T;
-    const uint32_t ostart = op + sn_excl_sum(len, T);
-    if (uint64_t(op) + T > ulen) return false;
-    const uint32_t in_frag = ostart & (kSnBlock - 1u);
-    // (one vector compare per ballot, the lane masks combined on the scalar unit; a lane that
-    // is no member has len 0)
-    const uint64_t crosses = sn_ballot(in_frag + len > kSnBlock);
-    // offset 0, or in front of the fragment
-    const uint64_t reaches = sn_ballot((mem ? ml : 0u) != 0u) & sn_ballot(in_frag <= off - 1u);
-    if (crosses | reaches) return false;
-    const uint64_t Fm = sn_ballot(len != 0u) & sn_ballot(in_frag == 0u) & sn_ballot(ostart != 0u);
-    if (__builtin_amdgcn_inverse_ballot_w64(Fm)) t->ip[ostart >> 16] = seg + uint32_t(lane);
-    found += uint32_t(__builtin_popcountll(Fm));
-    op = uni(op + T);
-    if (a_last == n) break;
-    ipn = a_last;
-    const uint32_t nseg = ipn & ~63u;
-    if (nseg == seg + 64u) {
-      cur = sn_parse_words(d, pf[0], n, nseg, lane);
-      pf[0] = pf[1];
-      pf[1] = pf[2];
-      pf[2] = pf[3];
-      pf[3] = sn_parse_load(d, nseg + 256u, lane);
-    } else {  // a literal ran over whole segments
-      cur = sn_parse(d, n, nseg, lane);
+      uint32_t w2[G], m2[G], p2[G];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pf[j] = sn_parse_load(d, nseg + 64u * uint32_t(j + 1), lane);
+      for (int g = 0; g < G; ++g) {
+        w2[g] = uint32_t(__builtin_amdgcn_ds_bpermute(int(P4[g]), int(W[g])));
+        m2[g] = uint32_t(__builtin_amdgcn_ds_bpermute(int(P4[g]), int(MX[g])));
+        p2[g] = uint32_t(__builtin_amdgcn_ds_bpermute(int(P4[g]), int(P4[g])));
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        W[g] += w2[g];
+        MX[g] = max(MX[g], m2[g]);
+        P4[g] = p2[g];
+      }
     }
-    seg = nseg;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint32_t seg = base + 64u * uint32_t(g);
+      if (more && (ipn & ~63u) == seg) {
+        const uint32_t x = ipn - seg;
+        const uint32_t last = uni(__builtin_amdgcn_readlane(P4[g], x)) >> 2;
+        const uint32_t T = uni(__builtin_amdgcn_readlane(W[g], x)) + uni(__builtin_amdgcn_readlane(L[g], last));
+        const uint32_t mx = uni(__builtin_amdgcn_readlane(MX[g], x));
+        const uint32_t a_last = uni(__builtin_amdgcn_readlane(c[g].A, last));
+        if (T > ulen - op || a_last > n) return false;  // (a poisoned length is beyond ulen)
+        const uint32_t in0 = op & (kSnBlock - 1u);
+        if ((in0 + T > kSnBlock) | (mx > in0)) {
+          if (!sn_scan_members(c[g], n, seg, x, op, t, found, lane)) return false;
+        } else if (in0 == 0u && op != 0u) {
+          if (lane == 0) t->ip[op >> 16] = ipn;
+          ++found;
+        }
+        op = uni(op + T);
+        ipn = a_last;
+        more = a_last != n;
+      }
+    }
+    const uint32_t nbase = ipn & ~63u;
+    if (more && nbase != base + 64u * uint32_t(G)) {  // a literal ran past the group
+#pragma unroll
+      for (int g = 0; g < G; ++g) pf[g] = sn_parse_load(d, nbase + 64u * uint32_t(g), lane);
+    }
+    base = nbase;
   }
   if (op != ulen || found != nfrag - 1u) return false;
   if (lane == 0) {

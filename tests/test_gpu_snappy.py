@@ -155,6 +155,39 @@ def test_uncompress_streams_that_do_not_split(engine, oracle_mod):
     assert _uncompress_batch(engine, streams) == want
 
 
+def test_uncompress_element_streams(engine, oracle_mod):
+    """streams assembled element by element (tests/snappy_streams.py): every tag kind and
+    literal-length encoding, lengths and offsets at their limits; fenced ones keep every element
+    and copy inside a 64 KiB fragment of the output (they decode by fragments), the others do
+    not, a quarter are damaged or cut short -- one batch, verdict and payload as the oracle's"""
+    from snappy_streams import FRAG, stream
+    rnd = random.Random(41)
+    streams = []
+    for it in range(240):
+        total = rnd.choice([rnd.randrange(1, 3000), rnd.randrange(FRAG - 300, FRAG + 300),
+                            rnd.randrange(FRAG, 4 * FRAG), 2 * FRAG, 3 * FRAG + 1])
+        st, _ = stream(rnd, total, rnd.random() < 0.6, rnd.random() < 0.2)
+        if it % 8 == 6:
+            b = bytearray(st)
+            for _ in range(rnd.randrange(1, 4)):
+                b[rnd.randrange(3, len(b)) if len(b) > 3 else 0] = rnd.getrandbits(8)
+            st = bytes(b)
+        elif it % 8 == 7 and len(st) > 4:
+            st = st[:rnd.randrange(3, len(st))]
+        n = oracle_mod.snappy_uncompressed_length(st)
+        if n is not None and n <= (1 << 23):
+            streams.append(st)
+    want = [oracle_mod.snappy_uncompress(s) for s in streams]
+    assert sum(w[0] == 0 for w in want) > 150 and sum(w[0] != 0 for w in want) > 20
+    res = _uncompress_batch(engine, streams)
+    for i, ((st, out), (err, exp)) in enumerate(zip(res, want)):
+        assert (st == 0) == (err == 0), (i, st, err)
+        if err == 0:
+            assert out == exp, i
+        else:
+            assert st == engine.SNAPPY_E_IO, (i, st)
+
+
 def test_uncompress_verdicts_on_damaged_streams(engine, oracle_mod):
     rnd = random.Random(9)
     base = [W.gen_json(5000, 4), bytes(3000) + W.gen_json(2000, 1), (rnd.randbytes(100) * 60)]

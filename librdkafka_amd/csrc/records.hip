@@ -13,8 +13,8 @@
 // Workgroups of 256 threads work on chunks of 256 records (grid = chunks x batches):
 //   sizes: a thread sizes one record (zig-zag varints, rdvarint.h:48-75), a chunk scan
 //          plus a per-batch scan of chunk totals place it -> record offsets, batch size;
-//   write: per chunk, record descriptors in LDS, then output-centric 16-byte pieces:
-//          coalesced aligned stores, 16 arena loads in flight per lane (v2_write_kernel).
+//   write: a thread writes its record's varints; key / value / header bytes are copied as
+//          16-byte tasks, one per lane, by the whole workgroup (v2_write_kernel).
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -188,32 +188,119 @@ __device__ __forceinline__ void st_be(uint8_t *p, uint64_t v, int n) {
 }
 
 // ---- write: grid (chunks, batches); chunk 0 also writes the header.
-// Phase 1, one lane per record: field widths and sources into LDS.  Phase 2, output-centric:
-// the chunk's output span is cut into 16-byte pieces aligned in the batch; a lane builds a
-// piece byte by byte (the record by a binary search of the chunk's record offsets, then the
-// field: varint byte, Attributes, or an arena byte -- every piece issues its 16 arena loads
-// at once) and writes it with one 16-byte store, coalesced across the wave.  Pieces cut by
-// the span ends (shared with the neighbouring chunk or the header) use byte stores.
-struct RecD {
-  uint64_t u[6];      // zig-zag values: L, T, O, K, V, H
-  uint64_t src[3];    // arena offsets: key, value, headers
-  uint32_t off;       // record start from the batch start
-  uint32_t end[10];   // field ends from the record start: L, attr, T, O, K, key, V, val, H, hdrs
+// Phase 1, one lane per record: the varints and Attributes (a tenth of the bytes), and key /
+// value / header bytes shorter than 16; longer ones become copy segments (destination, arena
+// offset, length) in LDS, cut into 16-byte tasks.
+// Phase 2, one lane per task: 16 bytes from the arena at byte alignment (one unaligned
+// dwordx4 load; consecutive tasks of a segment sit in consecutive lanes, so a wave reads
+// contiguous runs).  A segment's last task ends at the segment's end and overlaps the task
+// before it with the same bytes, so no task is partial.
+// Where the bytes go: memory takes whole aligned sectors well and everything else badly --
+// measured on this kernel, a byte store per lane to scattered records wrote 25 bytes to HBM
+// per byte stored, and 16-byte stores at byte alignment three times their size.  So a chunk
+// whose records fit kTile bytes (256 records of up to ~140 bytes) is put together in LDS by
+// both phases and then written with aligned 16-byte stores, every sector once.  A larger
+// chunk writes straight to memory.
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(3))) uint8_t rec_lds_u8;
+typedef __attribute__((address_space(3))) u32x4_a1 rec_lds_u32x4_a1;
+
+constexpr uint32_t kCopyTask = 16;  // bytes per task
+constexpr uint32_t kTile = 36864;   // LDS bytes for a chunk's records
+
+struct ToBatch {  // batch byte q in memory
+  uint8_t *bo;
+  __device__ __forceinline__ void st8(uint32_t q, uint32_t v) const { bo[q] = uint8_t(v); }
+  __device__ __forceinline__ void st16(uint32_t q, u32x4_a1 v) const {
+    *reinterpret_cast<u32x4_a1 *>(bo + q) = v;
+  }
+};
+struct ToTile {  // batch byte q in the tile, which starts at batch byte `first`
+  rec_lds_u8 *t;
+  uint32_t first;
+  __device__ __forceinline__ void st8(uint32_t q, uint32_t v) const { t[q - first] = uint8_t(v); }
+  __device__ __forceinline__ void st16(uint32_t q, u32x4_a1 v) const {
+    *reinterpret_cast<rec_lds_u32x4_a1 *>(t + (q - first)) = v;
+  }
 };
 
-__device__ __forceinline__ uint32_t piece_byte(const RecD &d, uint32_t t, uint64_t &src) {
-  // returns the byte value, or 0x100 when the byte is arena[src]
-  if (t < d.end[0]) return vbyte(d.u[0], t, d.end[0]);
-  if (t < d.end[1]) return 0u;  // Attributes (:722)
-  if (t < d.end[2]) return vbyte(d.u[1], t - d.end[1], d.end[2] - d.end[1]);
-  if (t < d.end[3]) return vbyte(d.u[2], t - d.end[2], d.end[3] - d.end[2]);
-  if (t < d.end[4]) return vbyte(d.u[3], t - d.end[3], d.end[4] - d.end[3]);
-  if (t < d.end[5]) { src = d.src[0] + (t - d.end[4]); return 0x100u; }
-  if (t < d.end[6]) return vbyte(d.u[4], t - d.end[5], d.end[6] - d.end[5]);
-  if (t < d.end[7]) { src = d.src[1] + (t - d.end[6]); return 0x100u; }
-  if (t < d.end[8]) return vbyte(d.u[5], t - d.end[7], d.end[8] - d.end[7]);
-  src = d.src[2] + (t - d.end[8]);
-  return 0x100u;
+template <class To>
+__device__ __forceinline__ uint32_t put_varint(const To &to, uint32_t q, uint64_t u, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) to.st8(q + i, vbyte(u, i, n));
+  return q + n;
+}
+
+struct WriteLds {
+  uint32_t last[kRecBlock];     // tasks of the records up to and including this one
+  uint32_t sdst[3][kRecBlock];  // a record's segments: key, value, headers
+  uint32_t slen[3][kRecBlock];  // (0: none)
+  uint64_t ssrc[3][kRecBlock];
+  uint32_t wsum[kRecBlock / 64];
+};
+
+// phases 1 and 2 of a chunk; r, off: this thread's record (threadIdx.x < nrec)
+template <class To>
+__device__ __forceinline__ void write_chunk(const To &to, const Msgs &m, WriteLds &L, const Rec &r,
+                                            uint32_t off, uint32_t msg, uint32_t nrec) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t mine = 0;  // this record's tasks
+  if (threadIdx.x < nrec) {
+    uint32_t q = put_varint(to, off, r.uL, r.sL);  // Length (:706)
+    to.st8(q++, 0u);                               // Attributes (:722)
+    q = put_varint(to, q, r.uT, r.sT);             // TimestampDelta (:725)
+    q = put_varint(to, q, r.uO, r.sO);             // OffsetDelta (:729)
+    const uint32_t flen[3] = {r.kb, r.vb, r.hb};
+    const uint64_t fu[3] = {r.uK, r.uV, r.uH};     // KeyLen, ValueLen, HeaderCount varints
+    const uint32_t fs[3] = {r.sK, r.sV, r.sH};
+    const uint64_t fsrc[3] = {r.kb ? m.key_off[msg] : 0, r.vb ? m.val_off[msg] : 0,
+                              r.hb ? m.hdr_off[msg] : 0};
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      q = put_varint(to, q, fu[f], fs[f]);
+      const uint32_t n = flen[f];
+      const bool seg = n >= kCopyTask;
+      if (!seg)
+        for (uint32_t i = 0; i < n; ++i) to.st8(q + i, m.arena[fsrc[f] + i]);
+      L.sdst[f][threadIdx.x] = q;
+      L.slen[f][threadIdx.x] = seg ? n : 0u;
+      L.ssrc[f][threadIdx.x] = fsrc[f];
+      mine += seg ? (n + kCopyTask - 1u) / kCopyTask : 0u;
+      q += n;
+    }
+  }
+  // tasks up to each record: scan over the workgroup
+  uint32_t x = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) L.wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < kRecBlock / 64; ++i) {
+    before += i < w ? L.wsum[i] : 0u;
+    total += L.wsum[i];
+  }
+  L.last[threadIdx.x] = before + x;
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < total; t += kRecBlock) {
+    uint32_t lo = 0, hi = nrec - 1u;  // the first record with last[rec] > t
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (L.last[mid] > t) hi = mid; else lo = mid + 1u;
+    }
+    const uint32_t rec = lo;
+    uint32_t k = t - (rec ? L.last[rec - 1u] : 0u);
+    const uint32_t n0 = (L.slen[0][rec] + kCopyTask - 1u) / kCopyTask;
+    const uint32_t n1 = (L.slen[1][rec] + kCopyTask - 1u) / kCopyTask;
+    const int f = k < n0 ? 0 : (k < n0 + n1 ? 1 : 2);
+    k -= f == 0 ? 0u : (f == 1 ? n0 : n0 + n1);
+    const uint32_t len = L.slen[f][rec];
+    const uint32_t o = min(k * kCopyTask, len - kCopyTask);
+    to.st16(L.sdst[f][rec] + o, *reinterpret_cast<const u32x4_a1 *>(m.arena + L.ssrc[f][rec] + o));
+  }
 }
 
 __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch *__restrict__ batches,
@@ -222,7 +309,8 @@ __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch
                                                             const int64_t *__restrict__ max_ts,
                                                             const uint64_t *__restrict__ out_offs,
                                                             uint8_t *__restrict__ out) {
-  __shared__ RecD D[kRecBlock];
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kTile];
+  __shared__ WriteLds L;
   __shared__ uint32_t span[2];
   const Batch b = batches[blockIdx.y];
   uint8_t *bo = out + out_offs[blockIdx.y];
@@ -245,76 +333,34 @@ __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch
   }
   if (c0 >= b.msg_count) return;
   const uint32_t nrec = b.msg_count - c0 < kRecBlock ? b.msg_count - c0 : kRecBlock;
-  // phase 1
+  Rec r = {};
+  uint32_t off = 0, msg = 0;
   if (threadIdx.x < nrec) {
-    const uint32_t k = c0 + threadIdx.x, msg = b.first_msg + k;
-    const Rec r = rec_fields(m, msg, k, m.ts[b.first_msg]);
-    RecD &d = D[threadIdx.x];
-    d.u[0] = r.uL; d.u[1] = r.uT; d.u[2] = r.uO; d.u[3] = r.uK; d.u[4] = r.uV; d.u[5] = r.uH;
-    d.src[0] = r.kb ? m.key_off[msg] : 0;
-    d.src[1] = r.vb ? m.val_off[msg] : 0;
-    d.src[2] = r.hb ? m.hdr_off[msg] : 0;
-    const uint32_t off = rec_offs[msg];
-    d.off = off;
-    uint32_t e = r.sL;
-    d.end[0] = e;
-    d.end[1] = e += 1u;
-    d.end[2] = e += r.sT;
-    d.end[3] = e += r.sO;
-    d.end[4] = e += r.sK;
-    d.end[5] = e += r.kb;
-    d.end[6] = e += r.sV;
-    d.end[7] = e += r.vb;
-    d.end[8] = e += r.sH;
-    d.end[9] = e += r.hb;
+    const uint32_t k = c0 + threadIdx.x;
+    msg = b.first_msg + k;
+    r = rec_fields(m, msg, k, m.ts[b.first_msg]);
+    off = rec_offs[msg];
     if (threadIdx.x == 0) span[0] = off;
-    if (threadIdx.x == nrec - 1u) span[1] = off + e;
+    if (threadIdx.x == nrec - 1u) span[1] = off + r.size;
   }
   __syncthreads();
-  // phase 2
   const uint32_t s0 = span[0], s1 = span[1];
-  // pieces are 16-byte aligned in memory (batch offsets are arbitrary)
-  const uint32_t q0 = s0 - uint32_t((reinterpret_cast<uintptr_t>(bo) + s0) & 15u);
-  for (uint32_t q = q0 + threadIdx.x * 16u; q < s1; q += kRecBlock * 16u) {
-    // record holding byte q (or the first record when q < s0)
-    uint32_t lo = 0, hi = nrec - 1u;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1u) >> 1;
-      if (D[mid].off <= q) lo = mid; else hi = mid - 1u;
-    }
-    uint32_t r = lo;
-    RecD dr = D[r];  // the current record's descriptor, in registers
-    uint32_t nxt = r + 1u < nrec ? D[r + 1u].off : 0xffffffffu;
-    uint32_t val[16];
-    uint64_t src[16];
-#pragma unroll
-    for (uint32_t u = 0; u < 16; ++u) {
-      const uint32_t p = q + u;
-      if (p >= nxt) {  // next record (records are >= 6 bytes: at most 3 per piece)
-        ++r;
-        dr = D[r];
-        nxt = r + 1u < nrec ? D[r + 1u].off : 0xffffffffu;
-      }
-      src[u] = 0;
-      val[u] = (p >= s0 && p < s1) ? piece_byte(dr, p - dr.off, src[u]) : 0x200u;
-    }
-    uint8_t byte[16];
-#pragma unroll
-    for (uint32_t u = 0; u < 16; ++u) byte[u] = m.arena[src[u]];  // all 16 loads in flight
-    uint32_t w[4] = {0, 0, 0, 0};
-    bool full = true;
-#pragma unroll
-    for (uint32_t u = 0; u < 16; ++u) {
-      const uint32_t v = val[u] == 0x100u ? uint32_t(byte[u]) : val[u];
-      full = full && val[u] != 0x200u;
-      w[u >> 2] |= (v & 0xffu) << (8u * (u & 3u));
-    }
-    if (full) {
-      *reinterpret_cast<uint4 *>(bo + q) = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-#pragma unroll
-      for (uint32_t u = 0; u < 16; ++u)
-        if (val[u] != 0x200u) bo[q + u] = uint8_t(w[u >> 2] >> (8u * (u & 3u)));
+  // the tile starts at the 16-byte boundary of memory at or in front of the chunk's first byte
+  const uint32_t mis = uint32_t((reinterpret_cast<uintptr_t>(bo) + s0) & 15u);
+  const uint32_t used = mis + (s1 - s0);
+  if (used > kTile) {
+    write_chunk(ToBatch{bo}, m, L, r, off, msg, nrec);
+    return;
+  }
+  write_chunk(ToTile{(rec_lds_u8 *)tile, s0 - mis}, m, L, r, off, msg, nrec);
+  __syncthreads();
+  uint8_t *g = bo + s0 - mis;
+  for (uint32_t i = threadIdx.x * 16u; i < used; i += kRecBlock * 16u) {
+    if (i >= mis && i + 16u <= used) {
+      *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(tile + i);
+    } else {  // the chunk's first and last piece: the neighbours' bytes stay
+      const uint32_t j0 = i > mis ? i : mis, j1 = i + 16u < used ? i + 16u : used;
+      for (uint32_t j = j0; j < j1; ++j) g[j] = tile[j];
     }
   }
 }

@@ -44,6 +44,53 @@ def test_v2_build_matches_oracle(engine, oracle_mod, headers):
         assert crcs[i] == int.from_bytes(exp[17:21], "big")
 
 
+def test_v2_build_record_size_mix(engine, oracle_mod):
+    """keys, values and header blocks of every length around the 16-byte copy unit, and records
+    large enough that a chunk of 256 leaves the on-chip tile (values of 1000 to 70000 bytes),
+    at every alignment of the arena and of the batch in the output"""
+    rnd = np.random.default_rng(5)
+    n = 2200
+    sizes_v = [0, 1, 2, 15, 16, 17, 31, 32, 33, 47, 48, 49, 100, 255, 256, 1000, 4096, 20000, 70000]
+    arena = bytearray(rnd.integers(0, 256, 3, dtype=np.uint8).tobytes())
+    m = {k: np.zeros(n, t) for k, t in (("ts", np.int64), ("key_off", np.uint64), ("key_len", np.int32),
+                                        ("val_off", np.uint64), ("val_len", np.int32),
+                                        ("hdr_off", np.uint64), ("hdr_len", np.uint32),
+                                        ("hdr_cnt", np.int32))}
+    for i in range(n):
+        m["ts"][i] = 1600000000000 + int(rnd.integers(-5, 40))
+        # the first 700 records stay small (chunks inside the tile), the rest mix in large ones
+        pool = sizes_v[:13] if i < 700 else sizes_v
+        kl = int(rnd.choice([-1, 0, 3, 15, 16, 17, 40, 200]))
+        vl = int(rnd.choice(pool)) if i % 9 else -1
+        m["key_len"][i] = kl
+        if kl > 0:
+            m["key_off"][i] = len(arena)
+            arena += rnd.integers(0, 256, kl, dtype=np.uint8).tobytes()
+        m["val_len"][i] = vl
+        if vl > 0:
+            m["val_off"][i] = len(arena)
+            arena += rnd.integers(0, 256, vl, dtype=np.uint8).tobytes()
+        if i % 4 == 0:  # one header, name "h", value of hv bytes (varint lengths as on the wire)
+            hv = int(rnd.choice([0, 5, 12, 13, 14, 60]))
+            h = bytes([2, ord("h"), hv << 1]) + rnd.integers(0, 256, hv, dtype=np.uint8).tobytes()
+            m["hdr_off"][i] = len(arena)
+            m["hdr_len"][i] = len(h)
+            m["hdr_cnt"][i] = 1
+            arena += h
+    m["arena"] = np.frombuffer(bytes(arena), np.uint8)
+    spec = [(0, 1), (1, 255), (256, 257), (513, 187), (700, 300), (1000, 1), (1001, 513), (1514, 686)]
+    b = _batches(spec)
+    out, offs, sizes, crcs = E.msgset_v2_build(_dev(m), b, crc=True)
+    host = bytes(out.cpu().numpy())
+    offs, sizes, crcs = offs.cpu().numpy(), sizes.cpu().numpy(), crcs.cpu().numpy().view(np.uint32)
+    for i, (first, cnt) in enumerate(spec):
+        exp = oracle_mod.msgset_v2_write(m, first, cnt, 1000 + i, i % 3, 7 * i - 1, 0)
+        got = host[offs[i]:offs[i] + sizes[i]]
+        assert len(got) == len(exp), (i, len(got), len(exp))
+        assert got == exp, (i, next(j for j in range(len(exp)) if got[j] != exp[j]))
+        assert crcs[i] == int.from_bytes(exp[17:21], "big")
+
+
 def test_v2_build_then_verify(engine):
     """The built batches pass the engine's own CRC verify (reader side)."""
     import torch

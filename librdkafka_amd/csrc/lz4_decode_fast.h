@@ -78,7 +78,27 @@ __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t idx) {
   return uint32_t(__builtin_amdgcn_ds_bpermute(int(idx << 2), int(v)));
 }
 
-// Write the pending piece into the history ring and to HBM.
+// Output reaches memory a whole kOutChunk at a time, from the history ring, as one aligned
+// 16-byte store per lane: memory takes whole sectors well and pieces of a few bytes at
+// arbitrary alignment badly (every partly written sector is first read back from HBM; the
+// decoder fetched four times its output that way).
+constexpr uint32_t kOutChunk = 1024;
+typedef uint32_t fd_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t fd_u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(3))) fd_u32x4 fd_lds_u32x4;
+typedef __attribute__((address_space(1))) fd_u32x4_a1 fd_g_u32x4;
+
+// ring -> memory: output [c0, c0 + n), c0 a multiple of kOutChunk, n <= kOutChunk
+__device__ __forceinline__ void fast_write_out(const FastDec &d, uint32_t c0, uint32_t n, int lane) {
+  const uint32_t o = c0 + 16u * uint32_t(lane), l16 = 16u * uint32_t(lane);
+  if (l16 + 16u <= n) {
+    *(fd_g_u32x4 *)(d.out + o) = *(fd_lds_u32x4 *)ring_at(d, o);
+  } else if (l16 < n) {  // the block's last, partial 16 bytes
+    for (uint32_t j = 0; j < n - l16; ++j) d.out[o + j] = *ring_at(d, o + j);
+  }
+}
+
+// Write the pending piece into the history ring, and the chunk it completes to HBM.
 __device__ __forceinline__ void fast_retire(FastDec &d, int lane) {
   __builtin_amdgcn_sched_barrier(0);  // keep the wait for the piece's loads down here
   // (the three values pass through empty asm statements: a select between fields of `d`
@@ -87,12 +107,10 @@ __device__ __forceinline__ void fast_retire(FastDec &d, int lane) {
   uint32_t a = d.plb, b = d.prb, c = d.pfb;
   asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
   const uint32_t v = d.plit ? a : (d.prk ? b : c);
-  if (uint32_t(lane) < d.pn) {
-    const uint32_t o = d.poc + uint32_t(lane);
-    *ring_at(d, o) = uint8_t(v);
-    d.out[o] = uint8_t(v);
-  }
+  if (uint32_t(lane) < d.pn) *ring_at(d, d.poc + uint32_t(lane)) = uint8_t(v);
   asm volatile("" ::: "memory");
+  // (a piece is at most 64 bytes: it completes at most one chunk)
+  if (((d.poc + d.pn) ^ d.poc) & ~(kOutChunk - 1u)) fast_write_out(d, d.poc & ~(kOutChunk - 1u), kOutChunk, lane);
   d.pn = 0;
 }
 
@@ -118,8 +136,9 @@ __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t src, uint32_t pc
   // a literal's position is in range of the input only with its tag taken off; a lane
   // without a byte (all ones) stays out of range either way
   d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, src ^ kLitTag, 0, 0);
-  // far history was stored >= kRing/64 pieces (>= 64 vector-memory ops) ago:
-  // with in-order vmcnt retirement it has completed, so no wait is needed
+  // far history left the ring for memory at least (kRing - kOutChunk) / 64 pieces (that many
+  // vector-memory loads, all waited for) ago: with in-order vmcnt retirement its store has
+  // completed, so no wait is needed
   d.pfb = d.out[(lit | rk) ? 0u : q];
   asm volatile("" ::: "memory");  // ring bytes stored by other lanes
   d.prb = *ring_at(d, q);
@@ -428,6 +447,7 @@ __device__ int decode_block_fast(uintptr_t src, uint32_t csize, uintptr_t dst, u
     op = op_new;
     if (done) {
       fast_retire(d, lane);
+      fast_write_out(d, op & ~(kOutChunk - 1u), op & (kOutChunk - 1u), lane);
       return int(op);
     }
     ipn = a_last;

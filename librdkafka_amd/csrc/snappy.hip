@@ -888,6 +888,30 @@ __device__ __forceinline__ void sn_set_out(SnDec &d, uintptr_t dst) {
                    uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(dst)))));
 }
 
+// Output reaches memory a whole kSnOutChunk at a time, from the history ring, as one 16-byte
+// store per lane (aligned when the destination is): memory takes whole sectors well and
+// pieces of a few bytes badly.
+constexpr uint32_t kSnOutChunk = 1024;
+typedef uint32_t sn_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t sn_u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(3))) sn_u32x4 sn_lds_u32x4;
+typedef __attribute__((address_space(1))) sn_u32x4_a1 sn_g_u32x4;
+
+// ring -> memory: output [c0, c0 + n), c0 a multiple of kSnOutChunk, n <= kSnOutChunk
+__device__ __forceinline__ void sn_write_out(const SnDec &d, uint32_t c0, uint32_t n, int lane) {
+  const uint32_t l16 = 16u * uint32_t(lane), o = c0 + l16;
+  if (l16 + 16u <= n) {
+    *(sn_g_u32x4 *)(d.out + o) = *(sn_lds_u32x4 *)(d.ring + (o & kSnRingMask));
+  } else if (l16 < n) {  // the last, partial 16 bytes
+    for (uint32_t j = 0; j < n - l16; ++j) d.out[o + j] = d.ring[(o + j) & kSnRingMask];
+  }
+}
+
+// the output's last, incomplete chunk
+__device__ __forceinline__ void sn_write_tail(const SnDec &d, uint32_t op, int lane) {
+  sn_write_out(d, op & ~(kSnOutChunk - 1u), op & (kSnOutChunk - 1u), lane);
+}
+
 __device__ __forceinline__ void sn_retire(SnDec &d, int lane) {
   __builtin_amdgcn_sched_barrier(0);  // keep the wait for the piece's loads down here
   // (through empty asm statements: a select between fields of `d` would otherwise become one
@@ -895,12 +919,11 @@ __device__ __forceinline__ void sn_retire(SnDec &d, int lane) {
   uint32_t a = d.plb, b = d.prb, c = d.pfb;
   asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
   const uint32_t v = d.plit ? a : (d.prk ? b : c);
-  if (uint32_t(lane) < d.pn) {
-    const uint32_t o = d.poc + uint32_t(lane);
-    d.ring[o & kSnRingMask] = uint8_t(v);
-    d.out[o] = uint8_t(v);
-  }
+  if (uint32_t(lane) < d.pn) d.ring[(d.poc + uint32_t(lane)) & kSnRingMask] = uint8_t(v);
   asm volatile("" ::: "memory");
+  // (a piece is at most 64 bytes: it completes at most one chunk)
+  if (((d.poc + d.pn) ^ d.poc) & ~(kSnOutChunk - 1u))
+    sn_write_out(d, d.poc & ~(kSnOutChunk - 1u), kSnOutChunk, lane);
   d.pn = 0;
 }
 
@@ -1099,6 +1122,7 @@ __device__ int sn_decode_elems(SnDec &d, uint32_t n, uint32_t ipn, uint32_t ulen
     op = op_new;
     if (done) {
       sn_retire(d, lane);
+      sn_write_tail(d, op, lane);
       return op == ulen ? 0 : SN_FAIL(20);  // eof && writer_check_length (:1403)
     }
     ipn = a_last;

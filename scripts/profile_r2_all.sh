@@ -11,4 +11,6 @@ bash $P lz4hc_compress_level12_1MiB_json "lz4hc_build_kernel,lz4hc_compress_bloc
 bash $P snappy_compress_1MiB_json "snappy_compress_fragments_kernel,snappy_assemble_kernel" --workload snappyc --partitions 256 --steps 3 --warmup 1 &&
 bash $P snappy_uncompress_1MiB_json "snappy_scan_kernel,snappy_uncompress_kernel" --workload snappyd --partitions 1024 --steps 3 --warmup 1 &&
 bash $P consumer_crc_verify_lz4f_decompress_1MiB "crc32c_msgset_v2_split_kernel,crc32c_msgset_v2_combine_kernel,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_seq_kernel,lz4f_finish_kernel" --workload consumer --partitions 1024 --steps 3 --warmup 1 &&
+bash $P v2_record_serialize_1MiB_json "v2_chunk_kernel,v2_batch_kernel,v2_fixup_kernel,v2_write_kernel" --workload serialize --partitions 256 --steps 5 --warmup 1 &&
+bash $P v2_record_index_1MiB_json "v2_index_spec_kernel" --workload index --partitions 256 --steps 5 --warmup 1 &&
 echo PROFILE_ALL_OK

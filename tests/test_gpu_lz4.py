@@ -197,6 +197,42 @@ def test_batch_compress_decompress_roundtrip(engine, oracle_mod):
         assert hdec[doffs[i]:doffs[i] + len(b)] == b, i
 
 
+def test_batch_decompress_unaligned_destinations(engine, oracle_mod):
+    """outputs at every byte alignment, capacity exactly the decoded size, guard bytes between
+    them: each frame's bytes arrive and nothing next to them is touched (the decoder writes its
+    output in 16-byte stores)"""
+    import torch
+    rnd = random.Random(77)
+    sizes = [1, 15, 16, 17, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 65535, 65536, 65537,
+             70001, 131072 + 5, 200003] + [rnd.randrange(1, 150000) for _ in range(29)]
+    inputs = [W.gen_json(n, 100 + i) if i % 4 else (rnd.randbytes(7) * (n // 7 + 1))[:n]
+              for i, n in enumerate(sizes)]
+    frames = [oracle_mod.rdk_lz4_compress(b)[1] for b in inputs]
+    fbuf, foffs = _pack(frames)
+    d_in = torch.frombuffer(fbuf, dtype=torch.uint8).cuda()
+    in_offs = torch.tensor(foffs, dtype=torch.int64, device="cuda")
+    in_lens = torch.tensor([len(f) for f in frames], dtype=torch.int32, device="cuda")
+    doffs, pos = [], 0
+    for i, b in enumerate(inputs):
+        pos += 1 + (i * 7) % 16          # a gap of 1..16 guard bytes: every alignment occurs
+        doffs.append(pos)
+        pos += len(b)
+    total = pos + 64
+    d_dec = torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda")
+    dec_offs = torch.tensor(doffs, dtype=torch.int64, device="cuda")
+    dec_caps = torch.tensor([len(b) for b in inputs], dtype=torch.int32, device="cuda")
+    dec_lens = torch.zeros(len(inputs), dtype=torch.int32, device="cuda")
+    status = torch.full((len(inputs),), 7, dtype=torch.int32, device="cuda")
+    engine.lz4f_decompress_batch(d_in, in_offs, in_lens, d_dec, dec_offs, dec_caps, dec_lens, status)
+    st, dl = status.cpu().numpy(), dec_lens.cpu().numpy()
+    host = bytes(d_dec.cpu().numpy())
+    want = bytearray(b"\xa5" * total)
+    for o, b in zip(doffs, inputs):
+        want[o:o + len(b)] = b
+    assert (st == 0).all() and (dl == [len(b) for b in inputs]).all()
+    assert host == bytes(want)
+
+
 def test_batch_decompress_dst_too_small(engine, oracle_mod):
     import torch
     data = W.gen_json(200000)

@@ -77,7 +77,7 @@ def test_v2_build_record_size_mix(engine, oracle_mod):
             m["hdr_len"][i] = len(h)
             m["hdr_cnt"][i] = 1
             arena += h
-    m["arena"] = np.frombuffer(bytes(arena), np.uint8)
+    m["arena"] = np.frombuffer(bytes(arena), np.uint8).copy()
     spec = [(0, 1), (1, 255), (256, 257), (513, 187), (700, 300), (1000, 1), (1001, 513), (1514, 686)]
     b = _batches(spec)
     out, offs, sizes, crcs = E.msgset_v2_build(_dev(m), b, crc=True)

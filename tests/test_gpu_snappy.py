@@ -188,6 +188,41 @@ def test_uncompress_element_streams(engine, oracle_mod):
             assert st == engine.SNAPPY_E_IO, (i, st)
 
 
+def test_uncompress_unaligned_destinations(engine, oracle_mod):
+    """outputs at every byte alignment with guard bytes between them (single- and
+    multi-fragment streams): the bytes arrive and nothing next to them is touched"""
+    import torch
+    rnd = random.Random(78)
+    sizes = [1, 15, 16, 17, 1023, 1024, 1025, 4097, 65535, 65536, 65537, 131072, 200003, 3 * 65536 + 9] + \
+            [rnd.randrange(1, 300000) for _ in range(26)]
+    inputs = [W.gen_json(n, 200 + i) if i % 4 else (rnd.randbytes(5) * (n // 5 + 1))[:n]
+              for i, n in enumerate(sizes)]
+    streams = [oracle_mod.snappy_compress(b) for b in inputs]
+    hbuf, hoffs = _pack(streams)
+    d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
+    in_offs = torch.tensor(hoffs, dtype=torch.int64, device="cuda")
+    in_lens = torch.tensor([len(b) for b in streams], dtype=torch.int32, device="cuda")
+    doffs, pos = [], 0
+    for i, b in enumerate(inputs):
+        pos += 1 + (i * 7) % 16
+        doffs.append(pos)
+        pos += len(b)
+    total = pos + 64
+    d_out = torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda")
+    out_offs = torch.tensor(doffs, dtype=torch.int64, device="cuda")
+    out_caps = torch.tensor([len(b) for b in inputs], dtype=torch.int32, device="cuda")
+    out_lens = torch.zeros(len(inputs), dtype=torch.int32, device="cuda")
+    status = torch.full((len(inputs),), 77, dtype=torch.int32, device="cuda")
+    engine.snappy_uncompress_batch(d_in, in_offs, in_lens, d_out, out_offs, out_caps, out_lens, status)
+    st, ol = status.cpu().numpy(), out_lens.cpu().numpy()
+    host = bytes(d_out.cpu().numpy())
+    want = bytearray(b"\xa5" * total)
+    for o, b in zip(doffs, inputs):
+        want[o:o + len(b)] = b
+    assert (st == 0).all() and (ol == [len(b) for b in inputs]).all()
+    assert host == bytes(want)
+
+
 def test_uncompress_verdicts_on_damaged_streams(engine, oracle_mod):
     rnd = random.Random(9)
     base = [W.gen_json(5000, 4), bytes(3000) + W.gen_json(2000, 1), (rnd.randbytes(100) * 60)]

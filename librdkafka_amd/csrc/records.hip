@@ -188,19 +188,19 @@ __device__ __forceinline__ void st_be(uint8_t *p, uint64_t v, int n) {
 }
 
 // ---- write: grid (chunks, batches); chunk 0 also writes the header.
-// Phase 1, one lane per record: the varints and Attributes (a tenth of the bytes), and key /
+// One lane per record writes the varints and Attributes (a tenth of the bytes), and key /
 // value / header bytes shorter than 16; longer ones become copy segments (destination, arena
-// offset, length) in LDS, cut into 16-byte tasks.
-// Phase 2, one lane per task: 16 bytes from the arena at byte alignment (one unaligned
-// dwordx4 load; consecutive tasks of a segment sit in consecutive lanes, so a wave reads
-// contiguous runs).  A segment's last task ends at the segment's end and overlaps the task
-// before it with the same bytes, so no task is partial.
+// offset, length) in LDS, cut into 16-byte tasks.  One lane per task then moves 16 bytes from
+// the arena at byte alignment (one unaligned dwordx4 load; consecutive tasks of a segment sit
+// in consecutive lanes, so a wave reads contiguous runs).  A segment's last task ends at the
+// segment's end and overlaps the task before it with the same bytes, so no task is partial.
 // Where the bytes go: memory takes whole aligned sectors well and everything else badly --
 // measured on this kernel, a byte store per lane to scattered records wrote 25 bytes to HBM
-// per byte stored, and 16-byte stores at byte alignment three times their size.  So a chunk
-// whose records fit kTile bytes (256 records of up to ~140 bytes) is put together in LDS by
-// both phases and then written with aligned 16-byte stores, every sector once.  A larger
-// chunk writes straight to memory.
+// per byte stored, and 16-byte stores at byte alignment three times their size.  So the
+// chunk's bytes are put together in LDS, kTile of them at a time (256 records of up to ~140
+// bytes are one tile; larger chunks take several passes, each over the records and tasks that
+// reach into its window), and each tile is written with aligned 16-byte stores, every sector
+// once.
 typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 typedef __attribute__((address_space(3))) uint8_t rec_lds_u8;
 typedef __attribute__((address_space(3))) u32x4_a1 rec_lds_u32x4_a1;
@@ -208,19 +208,29 @@ typedef __attribute__((address_space(3))) u32x4_a1 rec_lds_u32x4_a1;
 constexpr uint32_t kCopyTask = 16;  // bytes per task
 constexpr uint32_t kTile = 36864;   // LDS bytes for a chunk's records
 
-struct ToBatch {  // batch byte q in memory
-  uint8_t *bo;
-  __device__ __forceinline__ void st8(uint32_t q, uint32_t v) const { bo[q] = uint8_t(v); }
-  __device__ __forceinline__ void st16(uint32_t q, u32x4_a1 v) const {
-    *reinterpret_cast<u32x4_a1 *>(bo + q) = v;
-  }
-};
-struct ToTile {  // batch byte q in the tile, which starts at batch byte `first`
+struct ToTile {  // the whole chunk is in the tile, which starts at batch byte `first`
   rec_lds_u8 *t;
   uint32_t first;
   __device__ __forceinline__ void st8(uint32_t q, uint32_t v) const { t[q - first] = uint8_t(v); }
   __device__ __forceinline__ void st16(uint32_t q, u32x4_a1 v) const {
     *reinterpret_cast<rec_lds_u32x4_a1 *>(t + (q - first)) = v;
+  }
+};
+struct ToWindow {  // the tile holds batch bytes [first, first + kTile); others are dropped
+  rec_lds_u8 *t;
+  uint32_t first;
+  __device__ __forceinline__ void st8(uint32_t q, uint32_t v) const {
+    if (q - first < kTile) t[q - first] = uint8_t(v);
+  }
+  __device__ __forceinline__ void st16(uint32_t q, u32x4_a1 v) const {
+    const uint32_t a = q - first;  // (wraps for a byte in front of the window)
+    if (a <= kTile - kCopyTask) {
+      *reinterpret_cast<rec_lds_u32x4_a1 *>(t + a) = v;
+    } else if (a < kTile || a + (kCopyTask - 1u) < kTile) {  // cut by an end of the window
+#pragma unroll
+      for (uint32_t j = 0; j < kCopyTask; ++j)
+        if (a + j < kTile) t[a + j] = uint8_t(v[j >> 2] >> (8u * (j & 3u)));
+    }
   }
 };
 
@@ -231,44 +241,40 @@ __device__ __forceinline__ uint32_t put_varint(const To &to, uint32_t q, uint64_
 }
 
 struct WriteLds {
-  uint32_t last[kRecBlock];     // tasks of the records up to and including this one
-  uint32_t sdst[3][kRecBlock];  // a record's segments: key, value, headers
-  uint32_t slen[3][kRecBlock];  // (0: none)
+  uint32_t last[kRecBlock];      // tasks of the records up to and including this one
+  uint32_t roff[kRecBlock + 1];  // record starts from the batch start, then the chunk's end
+  uint32_t sdst[3][kRecBlock];   // a record's segments: key, value, headers
+  uint32_t slen[3][kRecBlock];   // (0: none)
   uint64_t ssrc[3][kRecBlock];
   uint32_t wsum[kRecBlock / 64];
 };
 
-// phases 1 and 2 of a chunk; r, off: this thread's record (threadIdx.x < nrec)
-template <class To>
-__device__ __forceinline__ void write_chunk(const To &to, const Msgs &m, WriteLds &L, const Rec &r,
-                                            uint32_t off, uint32_t msg, uint32_t nrec) {
+__device__ __forceinline__ uint32_t seg_tasks(uint32_t len) { return (len + kCopyTask - 1u) / kCopyTask; }
+
+// the records' segments and task counts into LDS; returns the chunk's tasks
+__device__ __forceinline__ uint32_t chunk_prepare(const Msgs &m, WriteLds &L, const Rec &r, uint32_t off,
+                                                  uint32_t msg, uint32_t nrec) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t mine = 0;  // this record's tasks
+  uint32_t mine = 0;
   if (threadIdx.x < nrec) {
-    uint32_t q = put_varint(to, off, r.uL, r.sL);  // Length (:706)
-    to.st8(q++, 0u);                               // Attributes (:722)
-    q = put_varint(to, q, r.uT, r.sT);             // TimestampDelta (:725)
-    q = put_varint(to, q, r.uO, r.sO);             // OffsetDelta (:729)
     const uint32_t flen[3] = {r.kb, r.vb, r.hb};
-    const uint64_t fu[3] = {r.uK, r.uV, r.uH};     // KeyLen, ValueLen, HeaderCount varints
     const uint32_t fs[3] = {r.sK, r.sV, r.sH};
     const uint64_t fsrc[3] = {r.kb ? m.key_off[msg] : 0, r.vb ? m.val_off[msg] : 0,
                               r.hb ? m.hdr_off[msg] : 0};
+    uint32_t q = off + r.sL + 1u + r.sT + r.sO;
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
-      q = put_varint(to, q, fu[f], fs[f]);
-      const uint32_t n = flen[f];
-      const bool seg = n >= kCopyTask;
-      if (!seg)
-        for (uint32_t i = 0; i < n; ++i) to.st8(q + i, m.arena[fsrc[f] + i]);
+      q += fs[f];
+      const bool seg = flen[f] >= kCopyTask;
       L.sdst[f][threadIdx.x] = q;
-      L.slen[f][threadIdx.x] = seg ? n : 0u;
+      L.slen[f][threadIdx.x] = seg ? flen[f] : 0u;
       L.ssrc[f][threadIdx.x] = fsrc[f];
-      mine += seg ? (n + kCopyTask - 1u) / kCopyTask : 0u;
-      q += n;
+      mine += seg ? seg_tasks(flen[f]) : 0u;
+      q += flen[f];
     }
+    L.roff[threadIdx.x] = off;
+    if (threadIdx.x == nrec - 1u) L.roff[nrec] = off + r.size;
   }
-  // tasks up to each record: scan over the workgroup
   uint32_t x = mine;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -285,7 +291,36 @@ __device__ __forceinline__ void write_chunk(const To &to, const Msgs &m, WriteLd
   }
   L.last[threadIdx.x] = before + x;
   __syncthreads();
-  for (uint32_t t = threadIdx.x; t < total; t += kRecBlock) {
+  return total;
+}
+
+// this thread's record: varints, Attributes and the fields that are no segments
+template <class To>
+__device__ __forceinline__ void chunk_small(const To &to, const Msgs &m, const Rec &r, uint32_t off,
+                                            uint32_t msg) {
+  uint32_t q = put_varint(to, off, r.uL, r.sL);  // Length (:706)
+  to.st8(q++, 0u);                               // Attributes (:722)
+  q = put_varint(to, q, r.uT, r.sT);             // TimestampDelta (:725)
+  q = put_varint(to, q, r.uO, r.sO);             // OffsetDelta (:729)
+  const uint32_t flen[3] = {r.kb, r.vb, r.hb};
+  const uint64_t fu[3] = {r.uK, r.uV, r.uH};     // KeyLen, ValueLen, HeaderCount varints
+  const uint32_t fs[3] = {r.sK, r.sV, r.sH};
+  const uint64_t fsrc[3] = {r.kb ? m.key_off[msg] : 0, r.vb ? m.val_off[msg] : 0,
+                            r.hb ? m.hdr_off[msg] : 0};
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    q = put_varint(to, q, fu[f], fs[f]);
+    if (flen[f] < kCopyTask)
+      for (uint32_t i = 0; i < flen[f]; ++i) to.st8(q + i, m.arena[fsrc[f] + i]);
+    q += flen[f];
+  }
+}
+
+// tasks [t0, t1) of the chunk, one per lane
+template <class To>
+__device__ __forceinline__ void chunk_tasks(const To &to, const Msgs &m, const WriteLds &L, uint32_t nrec,
+                                            uint32_t t0, uint32_t t1) {
+  for (uint32_t t = t0 + threadIdx.x; t < t1; t += kRecBlock) {
     uint32_t lo = 0, hi = nrec - 1u;  // the first record with last[rec] > t
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -293,13 +328,25 @@ __device__ __forceinline__ void write_chunk(const To &to, const Msgs &m, WriteLd
     }
     const uint32_t rec = lo;
     uint32_t k = t - (rec ? L.last[rec - 1u] : 0u);
-    const uint32_t n0 = (L.slen[0][rec] + kCopyTask - 1u) / kCopyTask;
-    const uint32_t n1 = (L.slen[1][rec] + kCopyTask - 1u) / kCopyTask;
+    const uint32_t n0 = seg_tasks(L.slen[0][rec]), n1 = seg_tasks(L.slen[1][rec]);
     const int f = k < n0 ? 0 : (k < n0 + n1 ? 1 : 2);
     k -= f == 0 ? 0u : (f == 1 ? n0 : n0 + n1);
     const uint32_t len = L.slen[f][rec];
     const uint32_t o = min(k * kCopyTask, len - kCopyTask);
     to.st16(L.sdst[f][rec] + o, *reinterpret_cast<const u32x4_a1 *>(m.arena + L.ssrc[f][rec] + o));
+  }
+}
+
+// tile -> memory: tile[lo, hi) to g[lo, hi), g + 0 aligned to 16; whole 16-byte pieces with
+// aligned stores, the cut ones (a chunk's first and last: the neighbours' bytes stay) bytewise
+__device__ __forceinline__ void tile_out(const uint8_t *tile, uint8_t *g, uint32_t lo, uint32_t hi) {
+  for (uint32_t i = threadIdx.x * 16u; i < hi; i += kRecBlock * 16u) {
+    if (i >= lo && i + 16u <= hi) {
+      *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(tile + i);
+    } else {
+      const uint32_t j0 = i > lo ? i : lo, j1 = i + 16u < hi ? i + 16u : hi;
+      for (uint32_t j = j0; j < j1; ++j) g[j] = tile[j];
+    }
   }
 }
 
@@ -311,7 +358,6 @@ __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch
                                                             uint8_t *__restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t tile[kTile];
   __shared__ WriteLds L;
-  __shared__ uint32_t span[2];
   const Batch b = batches[blockIdx.y];
   uint8_t *bo = out + out_offs[blockIdx.y];
   const uint32_t c0 = blockIdx.x * kRecBlock;
@@ -333,35 +379,78 @@ __global__ __launch_bounds__(kRecBlock) void v2_write_kernel(Msgs m, const Batch
   }
   if (c0 >= b.msg_count) return;
   const uint32_t nrec = b.msg_count - c0 < kRecBlock ? b.msg_count - c0 : kRecBlock;
+  const bool on = threadIdx.x < nrec;
   Rec r = {};
   uint32_t off = 0, msg = 0;
-  if (threadIdx.x < nrec) {
+  if (on) {
     const uint32_t k = c0 + threadIdx.x;
     msg = b.first_msg + k;
     r = rec_fields(m, msg, k, m.ts[b.first_msg]);
     off = rec_offs[msg];
-    if (threadIdx.x == 0) span[0] = off;
-    if (threadIdx.x == nrec - 1u) span[1] = off + r.size;
   }
-  __syncthreads();
-  const uint32_t s0 = span[0], s1 = span[1];
-  // the tile starts at the 16-byte boundary of memory at or in front of the chunk's first byte
+  const uint32_t total = chunk_prepare(m, L, r, off, msg, nrec);
+  const uint32_t s0 = L.roff[0], s1 = L.roff[nrec];
+  // the tiles start at the 16-byte boundary of memory at or in front of the chunk's first byte
   const uint32_t mis = uint32_t((reinterpret_cast<uintptr_t>(bo) + s0) & 15u);
   const uint32_t used = mis + (s1 - s0);
-  if (used > kTile) {
-    write_chunk(ToBatch{bo}, m, L, r, off, msg, nrec);
+  rec_lds_u8 *lt = (rec_lds_u8 *)tile;
+  if (used <= kTile) {
+    const ToTile to{lt, s0 - mis};
+    if (on) chunk_small(to, m, r, off, msg);
+    chunk_tasks(to, m, L, nrec, 0u, total);
+    __syncthreads();
+    tile_out(tile, bo + s0 - mis, mis, used);
     return;
   }
-  write_chunk(ToTile{(rec_lds_u8 *)tile, s0 - mis}, m, L, r, off, msg, nrec);
-  __syncthreads();
-  uint8_t *g = bo + s0 - mis;
-  for (uint32_t i = threadIdx.x * 16u; i < used; i += kRecBlock * 16u) {
-    if (i >= mis && i + 16u <= used) {
-      *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(tile + i);
-    } else {  // the chunk's first and last piece: the neighbours' bytes stay
-      const uint32_t j0 = i > mis ? i : mis, j1 = i + 16u < used ? i + 16u : used;
-      for (uint32_t j = j0; j < j1; ++j) g[j] = tile[j];
+  for (uint32_t w0 = 0; w0 < used; w0 += kTile) {
+    const uint32_t first = s0 - mis + w0, lim = first + kTile;
+    const ToWindow to{lt, first};
+    // records that reach into [first, lim): from the last one that starts at or before
+    // `first` to the last one that starts before `lim`
+    uint32_t lo = 0, hi = nrec - 1u;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1u) >> 1;
+      if (L.roff[mid] <= first) lo = mid; else hi = mid - 1u;
     }
+    const uint32_t r_lo = lo;
+    hi = nrec - 1u;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1u) >> 1;
+      if (L.roff[mid] < lim) lo = mid; else hi = mid - 1u;
+    }
+    const uint32_t r_hi = lo;
+    if (threadIdx.x >= r_lo && threadIdx.x <= r_hi) chunk_small(to, m, r, off, msg);
+    // their tasks, less those of the first record that end in front of the window and those
+    // of the last that start behind it (a record can be many windows long); one task of
+    // slack at either end, the window drops what lies outside
+    uint32_t ta = L.last[r_lo], tb = r_hi ? L.last[r_hi - 1u] : 0u;
+    {
+      uint32_t t = r_lo ? L.last[r_lo - 1u] : 0u;
+      for (int f = 0; f < 3; ++f) {
+        const uint32_t len = L.slen[f][r_lo], dst = L.sdst[f][r_lo], n = seg_tasks(len);
+        if (n && dst + len > first) {
+          const uint32_t k = dst >= first ? 0u : (first - dst) / kCopyTask;
+          ta = t + (k ? k - 1u : 0u);
+          break;
+        }
+        t += n;
+      }
+      t = L.last[r_hi];
+      for (int f = 2; f >= 0; --f) {
+        const uint32_t len = L.slen[f][r_hi], dst = L.sdst[f][r_hi], n = seg_tasks(len);
+        t -= n;
+        if (n && dst < lim) {
+          const uint32_t k = (lim - dst + kCopyTask - 1u) / kCopyTask + 1u;
+          tb = t + (k < n ? k : n);
+          break;
+        }
+      }
+    }
+    chunk_tasks(to, m, L, nrec, ta, tb);
+    __syncthreads();
+    const uint32_t rest = used - w0;
+    tile_out(tile, bo + first, w0 ? 0u : mis, rest < kTile ? rest : kTile);
+    __syncthreads();
   }
 }
 

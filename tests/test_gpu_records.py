@@ -46,8 +46,9 @@ def test_v2_build_matches_oracle(engine, oracle_mod, headers):
 
 def test_v2_build_record_size_mix(engine, oracle_mod):
     """keys, values and header blocks of every length around the 16-byte copy unit, and records
-    large enough that a chunk of 256 leaves the on-chip tile (values of 1000 to 70000 bytes),
-    at every alignment of the arena and of the batch in the output"""
+    large enough that a chunk of 256 takes many passes of the on-chip tile (values of 1000 to
+    70000 bytes, one of 1.5 MB that is many tiles long by itself), at every alignment of the
+    arena and of the batch in the output"""
     rnd = np.random.default_rng(5)
     n = 2200
     sizes_v = [0, 1, 2, 15, 16, 17, 31, 32, 33, 47, 48, 49, 100, 255, 256, 1000, 4096, 20000, 70000]
@@ -62,6 +63,8 @@ def test_v2_build_record_size_mix(engine, oracle_mod):
         pool = sizes_v[:13] if i < 700 else sizes_v
         kl = int(rnd.choice([-1, 0, 3, 15, 16, 17, 40, 200]))
         vl = int(rnd.choice(pool)) if i % 9 else -1
+        if i == 1600:
+            vl = 1500007
         m["key_len"][i] = kl
         if kl > 0:
             m["key_off"][i] = len(arena)

@@ -25,8 +25,12 @@
  *     writer sends the MessageSet uncompressed (rdkafka_msgset_writer.c:1175)
  *     and the reader raises a consumer error (rdkafka_msgset_reader.c:517-526);
  *   - crc32c / rd_slice_crc32c / rd_slice_crc32 return the checksum itself and
- *     have no error channel: a failed device call is retried once, then the
- *     process is aborted with a message rather than handed a wrong CRC.
+ *     have no error channel.  With no usable device the process is aborted with
+ *     a message.  With a device, a failed call (allocation, copy, launch) is
+ *     retried once; if that fails too, that one call's checksum is finished on
+ *     the host from the bytes already staged, reported on stderr the first time
+ *     and counted (rdk_hip_dropin_host_crcs), rather than handing back a wrong
+ *     CRC or taking the producer down.
  */
 #ifndef LIBRDKAFKA_HIP_H
 #define LIBRDKAFKA_HIP_H
@@ -100,6 +104,14 @@ rd_kafka_resp_err_t rd_kafka_lz4_decompress(rd_kafka_broker_t *rkb, int proper_h
  * library) verify that the writer's and reader's call sites bind to this library.  With
  * RDK_HIP_REPORT=1 in the environment the same counts are printed on stderr at exit. */
 void rdk_hip_dropin_calls(uint64_t out[5]);
+/* How many CRC drop-in calls finished on the host after the device path failed twice
+ * (see the error contract at the top).  0 in a healthy process; the GPU tests assert it. */
+uint64_t rdk_hip_dropin_host_crcs(void);
+/* Engine contexts created / destroyed so far.  Every calling thread gets one context (HIP
+ * stream, pinned staging, device scratch) on its first call; it is released when the
+ * thread exits, as librdkafka's broker threads do (rdkafka_broker.c:5082).  No
+ * counterpart in the reference. */
+void rdk_hip_ctx_counts(uint64_t out[2]);
 
 /* ---- snappy drop-ins (src/snappy.h).  Same signatures, return values and ownership as
  * the reference's definitions in src/snappy.c; the writer reaches them from

@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = (
     "rd_kafka_snappy_free_env", "rd_kafka_snappy_max_compressed_length",
     "rd_kafka_snappy_uncompressed_length", "rd_kafka_snappy_compress_iov",
     "rd_kafka_snappy_compress", "rd_kafka_snappy_uncompress", "rd_kafka_snappy_java_uncompress",
-    "rdk_hip_snappy_dropin_calls",
+    "rdk_hip_snappy_dropin_calls", "rdk_hip_dropin_host_crcs", "rdk_hip_ctx_counts",
 )
 
 
@@ -139,6 +139,10 @@ def lib():
     L.rdk_hip_msgset_v2_write.argtypes = [C.POINTER(_Msgs), vp, u32, vp, vp, vp, vp, vp, vp, vp]
     L.rdk_hip_msgset_v2_index.restype = i32
     L.rdk_hip_msgset_v2_index.argtypes = [vp] * 7 + [C.POINTER(_Rows), vp, u32, vp]
+    L.rdk_hip_dropin_host_crcs.restype = C.c_uint64
+    L.rdk_hip_dropin_host_crcs.argtypes = []
+    L.rdk_hip_ctx_counts.restype = None
+    L.rdk_hip_ctx_counts.argtypes = [vp]
     _lib = L
     return L
 
@@ -290,6 +294,18 @@ def rd_kafka_lz4_decompress(proper_hc: int, offset: int, frame) -> tuple[int, by
     res = C.string_at(out, n.value) if n.value else b""
     _libc().free(out)
     return 0, res
+
+
+def dropin_host_crcs() -> int:
+    """CRC drop-in calls that finished on the host after the device path failed twice."""
+    return int(lib().rdk_hip_dropin_host_crcs())
+
+
+def ctx_counts() -> tuple[int, int]:
+    """(created, destroyed) per-thread engine contexts."""
+    a = (C.c_uint64 * 2)()
+    lib().rdk_hip_ctx_counts(a)
+    return int(a[0]), int(a[1])
 
 
 _libc_h = None

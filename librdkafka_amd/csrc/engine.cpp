@@ -6,6 +6,7 @@
 // serialise on a shared lock.  CRC tables are uploaded once per device.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -21,6 +22,43 @@ int lz4f_noalloc_setup(int dev);  // lz4_decode.hip: per-device address of its s
 
 static thread_local char tl_err[512];
 static thread_local Ctx *tl_ctx = nullptr;
+
+// Releases everything a thread's context holds: its stream, pinned staging and device
+// scratch.  librdkafka creates and destroys broker threads as brokers come and go
+// (rdkafka_broker.c:5082), so a context must not outlive its thread.
+static void ctx_destroy(Ctx *c) {
+  if (!c) return;
+  if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->stream) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+  }
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  for (int i = 0; i < kScratchRegions; ++i) {
+    if (c->d_stage[i]) (void)hipFree(c->d_stage[i]);
+    if (c->d_done[i]) (void)hipEventDestroy(c->d_done[i]);
+  }
+  for (int i = 0; i < c->crc_streams; ++i)
+    if (c->crc_buf[i]) (void)hipFree(c->crc_buf[i]);
+  if (c->d_desc) (void)hipFree(c->d_desc);
+  if (c->h_desc) (void)hipHostFree(c->h_desc);
+  (void)hipGetLastError();
+  delete c;
+}
+
+// Owner of the calling thread's context: its destructor runs when the thread exits (for
+// the main thread: before the static destructors, so before the HIP runtime unloads).
+static std::atomic<uint64_t> g_ctx_created{0}, g_ctx_destroyed{0};
+struct CtxOwner {
+  ~CtxOwner() {
+    if (tl_ctx) {
+      ctx_destroy(tl_ctx);
+      tl_ctx = nullptr;
+      g_ctx_destroyed++;
+    }
+  }
+};
+static thread_local CtxOwner tl_owner;
 
 int set_error(int code, const char *fmt, ...) {
   va_list ap;
@@ -98,7 +136,11 @@ int bind(int dev) {
   int rc = upload_tables(dev);
   if (rc) return rc;
   if ((rc = lz4f_noalloc_setup(dev))) return rc;
-  if (!tl_ctx) tl_ctx = new Ctx();
+  if (!tl_ctx) {
+    (void)&tl_owner;  // odr-use: registers the thread-exit destructor
+    tl_ctx = new Ctx();
+    g_ctx_created++;
+  }
   if (tl_ctx->device != dev) {
     if (tl_ctx->stream) (void)hipStreamDestroy(tl_ctx->stream);
     tl_ctx->stream = nullptr;
@@ -140,22 +182,28 @@ static size_t grow(size_t have, size_t want) {
   return n;
 }
 
-int ensure_host(Ctx *c, size_t bytes) {
-  if (c->h_cap >= bytes) return 0;
-  if (c->h_stage) (void)hipHostFree(c->h_stage);
-  c->h_stage = nullptr;
-  size_t n = grow(c->h_cap, bytes);
-  RDK_HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&c->h_stage), n, hipHostMallocDefault));
-  c->h_cap = n;
-  return 0;
-}
-
 // Upper bound on any one device scratch region, from $RDK_HIP_MAX_SCRATCH_BYTES
 // (0 / unset = no bound): lets a deployment cap the engine's footprint and lets the
 // tests force the allocation-failure paths.
 static size_t scratch_limit() {
   const char *e = getenv("RDK_HIP_MAX_SCRATCH_BYTES");
   return e ? size_t(strtoull(e, nullptr, 10)) : 0;
+}
+
+int ensure_host(Ctx *c, size_t bytes) {
+  if (c->h_cap >= bytes) return 0;
+  // grow-only; the old contents are NOT kept: callers size the staging before they fill it
+  size_t n = grow(c->h_cap, bytes);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  c->h_stage = nullptr;
+  c->h_cap = 0;  // a failed allocation must not leave a capacity behind a null pointer
+  const size_t lim = scratch_limit();
+  if (lim && n > lim)
+    return set_error(RDK_HIP_E_NOMEM, "pinned staging of %zu bytes exceeds RDK_HIP_MAX_SCRATCH_BYTES=%zu",
+                     n, lim);
+  RDK_HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&c->h_stage), n, hipHostMallocDefault));
+  c->h_cap = n;
+  return 0;
 }
 
 static int dev_alloc(uint8_t **p, size_t n) {
@@ -268,6 +316,12 @@ const uint32_t *crc_x2n_dev(int device, int kind) { return g_x2n[kind][device]; 
 RDK_API int rdk_hip_init(int device) {
   if (device < 0) device = rdk::default_device();
   return rdk::bind(device);
+}
+
+// contexts created / destroyed so far (one per calling thread; destroyed at thread exit)
+RDK_API void rdk_hip_ctx_counts(uint64_t out[2]) {
+  out[0] = rdk::g_ctx_created.load();
+  out[1] = rdk::g_ctx_destroyed.load();
 }
 
 RDK_API const char *rdk_hip_last_error(void) { return rdk::last_error(); }

@@ -429,7 +429,8 @@ struct DevReader {
 // Also appends the (frame, block) items of every regular frame to a compact
 // work list, so the block kernel's wavefronts only ever see real blocks.
 __global__ void lz4f_walk_kernel(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
-                                 const uint32_t *__restrict__ in_lens, uint32_t n,
+                                 const uint32_t *__restrict__ in_lens,
+                                 const uint32_t *__restrict__ out_caps, uint32_t n,
                                  FrameState *__restrict__ fs, BlockDesc *__restrict__ bd,
                                  uint32_t *__restrict__ work_count, uint32_t *__restrict__ work) {
   const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
@@ -438,15 +439,21 @@ __global__ void lz4f_walk_kernel(const uint8_t *__restrict__ in, const uint64_t 
   wk.header();
   BlockInfo b;
   uint32_t k = 0;
+  uint64_t last_most = 0;
   while (wk.next(b)) {
     if (k < uint32_t(kMaxDesc)) {
       bd[size_t(f) * kMaxDesc + k].b = b;
       bd[size_t(f) * kMaxDesc + k].result = 0;
     }
+    last_most = lz4f_block_most(b, wk.fi.max_block);
     ++k;
   }
   wk.fi.nblocks = k < uint32_t(kMaxDesc) ? k : uint32_t(kMaxDesc);
   if ((wk.fi.flags & F_LINKED) || k > uint32_t(kMaxDesc)) wk.fi.flags |= F_SEQ;
+  // Independent blocks decode in place at k * max_block.  A capacity that cannot hold that
+  // layout (a caller that sized the output from what the blocks can yield, for a frame of
+  // many short blocks) is decoded in stream order by one wavefront instead.
+  if (k && uint64_t(k - 1) * wk.fi.max_block + last_most > out_caps[f]) wk.fi.flags |= F_SEQ;
   fs[f].fi = wk.fi;
   fs[f].seq_result = 0;
   if (wk.fi.status == 0 && !(wk.fi.flags & (F_SKIPPABLE | F_SEQ)) && wk.fi.nblocks) {
@@ -681,7 +688,7 @@ void launch_decode(uint8_t *scratch, const uint8_t *d_in, const uint64_t *d_in_o
   uint32_t *work_count = reinterpret_cast<uint32_t *>(scratch + fs_bytes + bd_bytes);
   uint32_t *work = work_count + 64;
   hipLaunchKernelGGL(lz4f_walk_kernel, dim3((n + 63) / 64), dim3(64), 0, s, d_in, d_in_offs,
-                     d_in_lens, n, fs, bd, work_count, work);
+                     d_in_lens, d_out_caps, n, fs, bd, work_count, work);
   // persistent grid: as many workgroups per CU as the LDS rings and the 32 wave slots allow
   constexpr unsigned kWgPerCu = (160u * 1024u) / (kDecWaves * (kRing + 128u)) < 32u / kDecWaves
                                     ? (160u * 1024u) / (kDecWaves * (kRing + 128u))

@@ -52,6 +52,14 @@ struct BlockInfo {
   uint32_t xxh;      // stored block checksum (B_XXH)
 };
 
+// The most bytes a block can decode to: a stored block yields its own bytes; a compressed
+// block of c bytes at most 255 * c (each 255-run byte of a match length adds 255 bytes of
+// output), and never more than the frame's block size.
+RDK_HD inline uint64_t lz4f_block_most(const BlockInfo &b, uint32_t max_block) {
+  const uint64_t most = (b.flags & B_RAW) ? uint64_t(b.csize) : uint64_t(b.csize) * 255u;
+  return most < max_block ? most : max_block;
+}
+
 template <typename Rd>
 struct FrameWalker {
   Rd rd;            // byte reader: rd(i) -> byte i of the frame

@@ -134,7 +134,21 @@ int lz4f_decompress_host(Ctx *c, int proper_hc, uint8_t *in, size_t inlen, void 
   wk.header();
   BlockInfo b;
   uint64_t cap = 0;
-  while (wk.next(b)) cap += (b.flags & B_RAW) ? b.csize : wk.fi.max_block;
+  // Two sizings: `tight` = what the blocks can yield at most (lz4f_block_most), `slots` =
+  // the in-place layout of independent blocks (block k at k * max_block).  The slot layout
+  // is used when it costs at most 4x the tight bound (+ 1 MiB): every frame the reference's
+  // writer makes.  A small frame of many short blocks of a large block class would
+  // otherwise ask for gigabytes of staging; it gets the tight size and the device decodes
+  // it in stream order.
+  uint64_t tight = 0, slots = 0, last_most = 0;
+  uint32_t nb = 0;
+  while (wk.next(b)) {
+    last_most = lz4f_block_most(b, wk.fi.max_block);
+    tight += last_most;
+    ++nb;
+  }
+  if (nb) slots = uint64_t(nb - 1) * wk.fi.max_block + last_most;
+  cap = (slots <= 4 * tight + (1u << 20)) ? (slots > tight ? slots : tight) : tight;
   if (wk.fi.status) return wk.fi.status;
   if (cap > 0xFFFFFFF0ull) return RDK_HIP_RESP_ERR__CRIT_SYS_RESOURCE;
   const size_t in_bytes = (inlen + 255) & ~size_t(255);
@@ -166,13 +180,13 @@ int lz4f_decompress_host(Ctx *c, int proper_hc, uint8_t *in, size_t inlen, void 
   std::memcpy(&status, c->h_desc + 68, 4);
   if (status == kErrDstSize) return set_error(RDK_HIP_E_HIP, "lz4f decompress: output sizing");
   if (status) return status;
-  uint8_t *o = static_cast<uint8_t *>(std::malloc(olen ? olen : 1));
-  if (!o) return RDK_HIP_RESP_ERR__CRIT_SYS_RESOURCE;
-  if (olen) {
+  if (olen) {  // the copy first: nothing is owned yet if it fails
     RDK_HIP_CHECK(hipMemcpyAsync(c->h_stage, d_out, olen, hipMemcpyDeviceToHost, c->stream));
     RDK_HIP_CHECK(hipStreamSynchronize(c->stream));
-    std::memcpy(o, c->h_stage, olen);
   }
+  uint8_t *o = static_cast<uint8_t *>(std::malloc(olen ? olen : 1));
+  if (!o) return RDK_HIP_RESP_ERR__CRIT_SYS_RESOURCE;
+  if (olen) std::memcpy(o, c->h_stage, olen);
   *out = o;
   *outlen = olen;
   return 0;

@@ -11,8 +11,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "common.h"
+#include "crc32c_tables.h"
 #include "lz4_engine.h"
 #include "rdbuf_abi.h"
 
@@ -38,8 +41,10 @@ static int crc_staged(Ctx *c, size_t len, uint32_t init, uint32_t *out, int kind
   return 0;
 }
 
-// how often each drop-in symbol was entered (rdk_hip_dropin_calls)
+// how often each drop-in symbol was entered (rdk_hip_dropin_calls), and how often a CRC
+// symbol had to finish on the host after the device failed twice (rdk_hip_dropin_host_crcs)
 static std::atomic<uint64_t> g_calls[5];
+static std::atomic<uint64_t> g_host_crcs{0};
 enum { CALL_CRC32C = 0, CALL_SLICE_CRC32C, CALL_SLICE_CRC32, CALL_LZ4C, CALL_LZ4D };
 
 // RDK_HIP_REPORT=1: one line on stderr at process exit with the call counts, so a preload
@@ -48,10 +53,10 @@ __attribute__((destructor)) static void report_calls() {
   const char *e = getenv("RDK_HIP_REPORT");
   if (!e || !atoi(e)) return;
   fprintf(stderr, "librdkafka_hip: calls crc32c=%llu rd_slice_crc32c=%llu rd_slice_crc32=%llu "
-                  "rd_kafka_lz4_compress=%llu rd_kafka_lz4_decompress=%llu\n",
+                  "rd_kafka_lz4_compress=%llu rd_kafka_lz4_decompress=%llu host_crcs=%llu\n",
           (unsigned long long)g_calls[0].load(), (unsigned long long)g_calls[1].load(),
           (unsigned long long)g_calls[2].load(), (unsigned long long)g_calls[3].load(),
-          (unsigned long long)g_calls[4].load());
+          (unsigned long long)g_calls[4].load(), (unsigned long long)g_host_crcs.load());
 }
 
 static Ctx *ctx_or_die(const char *who) {
@@ -60,18 +65,45 @@ static Ctx *ctx_or_die(const char *who) {
   return c;
 }
 
-// Stage `len` bytes already gathered in c->h_stage and CRC them.  The CRC symbols
-// return the checksum itself, so they have no way to report a device error: a failed
-// attempt is retried once after draining the device (a transient allocation or launch
-// failure), and only a second failure aborts, loudly.
-static uint32_t crc_or_die(Ctx *c, size_t len, uint32_t init, int kind, const char *who) {
+// Byte-at-a-time CRC over host bytes with the table the device images are built from
+// (crc_build_tables: table 0 is the plain byte table of the polynomial).  Only the CRC
+// symbols' last resort below uses it.
+static uint32_t crc_host_bytes(const uint8_t *p, size_t len, uint32_t init, int kind) {
+  static uint32_t tab[2][256];
+  static std::once_flag once[2];
+  std::call_once(once[kind], [kind] {
+    std::vector<uint32_t> image(kCrcTableWords);
+    crc_build_tables(image.data(), kind == kCrcKind32 ? kCrc32Poly : kCrcPoly);
+    std::memcpy(tab[kind], image.data(), sizeof tab[kind]);
+  });
+  uint32_t c = ~init;
+  for (size_t i = 0; i < len; ++i) c = tab[kind][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+  return ~c;
+}
+
+// Stage `len` bytes already gathered in `bytes` (c->h_stage when the pinned staging could be
+// had) and CRC them.  The CRC symbols return the checksum itself, so they have no way to
+// report a device error: a failed attempt is retried once after draining the device (a
+// transient allocation or launch failure).  If that fails too the checksum of THIS call is
+// finished on the host from the staged bytes -- reported on stderr the first time and
+// counted (rdk_hip_dropin_host_crcs) -- because neither a wrong CRC nor taking the
+// producer down is acceptable for a per-call device error.  A process with no usable
+// gfx950 device never gets here: ctx_or_die() stops it.
+static uint32_t crc_or_host(Ctx *c, const uint8_t *bytes, size_t len, uint32_t init, int kind,
+                            const char *who) {
   uint32_t out = 0;
-  if (crc_staged(c, len, init, &out, kind) == 0) return out;
-  fprintf(stderr, "librdkafka_hip: %s: %s; retrying\n", who, last_error());
-  (void)hipDeviceSynchronize();
+  if (bytes == c->h_stage && c->h_stage) {
+    if (crc_staged(c, len, init, &out, kind) == 0) return out;
+    fprintf(stderr, "librdkafka_hip: %s: %s; retrying\n", who, last_error());
+    (void)hipDeviceSynchronize();
+    (void)hipGetLastError();
+    if (crc_staged(c, len, init, &out, kind) == 0) return out;
+  }
+  if (!g_host_crcs.fetch_add(1))
+    fprintf(stderr, "librdkafka_hip: %s: device path failed twice (%s); this call's checksum is "
+                    "computed on the host (counted in rdk_hip_dropin_host_crcs)\n", who, last_error());
   (void)hipGetLastError();
-  if (crc_staged(c, len, init, &out, kind)) fatal(who);
-  return out;
+  return crc_host_bytes(bytes, len, init, kind);
 }
 
 // The LZ4 symbols do have an error channel (rdkafka_lz4.c returns
@@ -106,13 +138,16 @@ RDK_API void rdk_hip_dropin_calls(uint64_t out[5]) {
   for (int i = 0; i < 5; ++i) out[i] = g_calls[i].load();
 }
 
+RDK_API uint64_t rdk_hip_dropin_host_crcs(void) { return g_host_crcs.load(); }
+
 RDK_API uint32_t crc32c(uint32_t crc, const void *buf, size_t len) {
   g_calls[CALL_CRC32C]++;
   Ctx *c = ctx_or_die("crc32c");
   if (len == 0) return crc;  // pre/post inversions cancel (crc32c.c:102,133)
-  if (ensure_host(c, len)) fatal("crc32c: pinned staging");
+  if (ensure_host(c, len))  // no pinned staging: nothing to copy from, finish on the host
+    return crc_or_host(c, static_cast<const uint8_t *>(buf), len, crc, kCrcKind32C, "crc32c");
   std::memcpy(c->h_stage, buf, len);
-  return crc_or_die(c, len, crc, kCrcKind32C, "crc32c");
+  return crc_or_host(c, c->h_stage, len, crc, kCrcKind32C, "crc32c");
 }
 
 // iovec gather (the rdbuf.c:1099-1101 / :1118-1119 loops) into the pinned staging buffer;
@@ -120,14 +155,23 @@ RDK_API uint32_t crc32c(uint32_t crc, const void *buf, size_t len) {
 static uint32_t slice_crc(rd_slice_t *slice, int kind, const char *who) {
   Ctx *c = ctx_or_die(who);
   const size_t total = slice_remains(slice);
-  if (ensure_host(c, total ? total : 1)) fatal(who);
   size_t of = 0, rlen;
   const void *p;
+  if (ensure_host(c, total ? total : 1)) {
+    // no pinned staging: chain the segments on the host, as rdbuf.c:1118-1119 does
+    if (!g_host_crcs.fetch_add(1))
+      fprintf(stderr, "librdkafka_hip: %s: %s; this call's checksum is computed on the host "
+                      "(counted in rdk_hip_dropin_host_crcs)\n", who, last_error());
+    uint32_t crc = 0;
+    while ((rlen = slice_reader(slice, &p)))
+      crc = crc_host_bytes(static_cast<const uint8_t *>(p), rlen, crc, kind);
+    return crc;
+  }
   while ((rlen = slice_reader(slice, &p))) {
     std::memcpy(c->h_stage + of, p, rlen);
     of += rlen;
   }
-  return crc_or_die(c, of, 0u, kind, who);
+  return crc_or_host(c, c->h_stage, of, 0u, kind, who);
 }
 
 RDK_API uint32_t rd_slice_crc32c(rd_slice_t *slice) {

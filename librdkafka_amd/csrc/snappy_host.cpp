@@ -47,9 +47,10 @@ static int sn_compress_staged(Ctx *c, size_t len, size_t *outlen) {
   const size_t bound = snappy_max_compressed_length(len);
   const size_t in_bytes = (len + 255) & ~size_t(255);
   int rc;
-  if ((rc = ensure_dev(c, 0, in_bytes + bound + 64)) || (rc = ensure_desc(c, 64)) ||
-      (rc = ensure_host(c, bound)))
-    return rc;
+  // the caller sized the pinned staging for `bound` BEFORE gathering the input into it
+  // (ensure_host does not keep contents when it grows)
+  if (c->h_cap < bound) return set_error(RDK_HIP_E_INVAL, "snappy staging smaller than the bound");
+  if ((rc = ensure_dev(c, 0, in_bytes + bound + 64)) || (rc = ensure_desc(c, 64))) return rc;
   uint8_t *d_in = c->d_stage[0], *d_out = c->d_stage[0] + in_bytes;
   uint64_t *hd = reinterpret_cast<uint64_t *>(c->h_desc);
   hd[0] = 0;
@@ -163,7 +164,10 @@ RDK_API int rd_kafka_snappy_compress_iov(struct snappy_env *env, const struct io
     sn_report("rd_kafka_snappy_compress_iov");
     return -EIO;
   }
-  int rc = ensure_host(c, input_length ? input_length : 1);
+  // one sizing for both uses of the staging: the gathered input now, the stream later
+  int rc = input_length >= 0x80000000ull
+               ? set_error(RDK_HIP_E_INVAL, "snappy input too large")
+               : ensure_host(c, snappy_max_compressed_length(input_length));
   size_t of = 0;
   for (size_t i = 0; !rc && i < iov_in_cnt && of < input_length; i++) {
     const size_t take = iov_in[i].iov_len < input_length - of ? iov_in[i].iov_len : input_length - of;
@@ -197,7 +201,11 @@ RDK_API int rd_kafka_snappy_uncompress(const char *compressed, size_t n, char *u
   g_sn_calls[1]++;
   uint32_t ulen;
   const uint8_t *in = reinterpret_cast<const uint8_t *>(compressed);
-  if (n >= 0x80000000ull || !sn_varint(in, n, &ulen)) {
+  // a literal-free stream expands by at most 64/3 per byte (a 3-byte copy element yields
+  // up to 64 bytes); anything declared beyond that, or beyond the 31 bits the engine
+  // handles, is refused before any staging is sized from the untrusted preamble
+  if (n >= 0x80000000ull || !sn_varint(in, n, &ulen) || ulen > 0x7FFFFFF0u ||
+      uint64_t(ulen) > uint64_t(n) * 22u + 64u) {
     // read_uncompressed_length accepts a fifth byte up to 127 where the strict parse does
     // not; such a preamble declares more than the 31 bits the engine handles
     return -EIO;

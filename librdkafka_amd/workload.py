@@ -146,3 +146,59 @@ def msgset_v01_bytes(msgs: dict, first: int, cnt: int, magic: int = 1,
         out += struct.pack(">i", kl if kl >= 0 else -1) + arena[ko:ko + kb].tobytes()
         out += struct.pack(">i", vl if vl >= 0 else -1) + arena[vo:vo + vb].tobytes()
     return bytes(out)
+
+
+PERF_PATTERN = b"librdkafka_performance testing!"   # examples/rdkafka_performance.c:798
+
+
+def gen_perf_messages(n: int, msgsize: int = 100, msgs_per_ms: int = 800) -> dict:
+    """The messages of `rdkafka_performance -P -s msgsize -c n`: every value is the pattern
+    repeated to msgsize bytes (examples/rdkafka_performance.c:1318-1325; all messages share
+    the one payload buffer), no key, no headers; timestamps are the produce() wall clock,
+    here advancing one millisecond every `msgs_per_ms` messages."""
+    value = (PERF_PATTERN * (msgsize // len(PERF_PATTERN) + 1))[:msgsize]
+    z32, z64 = np.zeros(n, np.int32), np.zeros(n, np.uint64)
+    return {"arena": np.frombuffer(value or b"\0", np.uint8).copy(),
+            "ts": 1600000000000 + np.arange(n, dtype=np.int64) // msgs_per_ms,
+            "key_off": z64.copy(), "key_len": np.full(n, -1, np.int32),
+            "val_off": z64.copy(), "val_len": np.full(n, msgsize, np.int32),
+            "hdr_off": z64.copy(), "hdr_len": np.zeros(n, np.uint32), "hdr_cnt": z32.copy()}
+
+
+def _zz_width(v: int) -> int:
+    u = ((v << 1) ^ (v >> 63)) & ((1 << 64) - 1)
+    w = 1
+    while u > 0x7F:
+        u >>= 7
+        w += 1
+    return w
+
+
+def perf_batches(msgs: dict, batch_num_messages: int = 10000, message_max_bytes: int = 1000000,
+                 request_overhead: int = 55) -> list[tuple[int, int]]:
+    """(first, count) of the MessageSets rd_kafka_msgset_writer_write_msgq
+    (rdkafka_msgset_writer.c:804-902) cuts a toppar's queue into: a batch ends at
+    batch.num.messages (rdkafka_conf.c:1155) or when the request buffer so far plus the next
+    message's estimated wire size (value + key + RD_KAFKAP_MESSAGE_V2_OVERHEAD = 36,
+    rdkafka_proto.h:508-524) would pass message.max.bytes (:859-863).  `request_overhead` is
+    the ProduceRequest framing in front of the MessageSet (55 bytes for topic "perftest",
+    client.id "rdkafka", ApiVersion 7)."""
+    n = len(msgs["ts"])
+    out, first = [], 0
+    while first < n:
+        length = request_overhead + V2_HEADER
+        cnt = 0
+        base_ts = int(msgs["ts"][first])
+        while first + cnt < n and cnt < batch_num_messages:
+            m = first + cnt
+            kl, vl = int(msgs["key_len"][m]), int(msgs["val_len"][m])
+            if cnt > 0 and length + 36 + max(kl, 0) + max(vl, 0) > message_max_bytes:
+                break
+            body = (1 + _zz_width(int(msgs["ts"][m]) - base_ts) + _zz_width(cnt) + _zz_width(kl) +
+                    max(kl, 0) + _zz_width(vl) + max(vl, 0) + _zz_width(int(msgs["hdr_cnt"][m])) +
+                    int(msgs["hdr_len"][m]))
+            length += _zz_width(body) + body
+            cnt += 1
+        out.append((first, cnt))
+        first += cnt
+    return out

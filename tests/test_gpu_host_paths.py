@@ -1,0 +1,134 @@
+"""Host-side paths of the drop-in symbols on a GPU box: contexts released at thread exit,
+the CRC symbols' last resort when the device path fails, output sizing of
+rd_kafka_lz4_decompress for frames of many short blocks, and the snappy drop-ins around
+the sizes at which the pinned staging grows."""
+import os
+import struct
+import subprocess
+import sys
+import textwrap
+import threading
+
+import pytest
+
+from librdkafka_amd import workload as W
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_thread_context_is_released_at_thread_exit(engine, oracle_mod):
+    """librdkafka creates and destroys broker threads (rdkafka_broker.c:5082): each one's
+    engine context (stream, pinned staging, device scratch) must go with it."""
+    data = W.gen_json(50000, 5)
+    want = oracle_mod.crc32c(0, data)
+    c0, d0 = engine.ctx_counts()
+    got = []
+
+    def broker_thread():
+        got.append(engine.crc32c(0, data))
+        err, fr = engine.rd_kafka_lz4_compress(1, 0, data)
+        got.append((err, engine.rd_kafka_lz4_decompress(1, 0, fr)))
+
+    for _ in range(6):
+        t = threading.Thread(target=broker_thread)
+        t.start()
+        t.join()
+    c1, d1 = engine.ctx_counts()
+    assert c1 - c0 == 6 and d1 - d0 == 6, (c0, d0, c1, d1)
+    for i in range(6):
+        assert got[2 * i] == want
+        assert got[2 * i + 1] == (0, (0, data))
+    assert engine.dropin_host_crcs() == 0
+
+
+def test_crc_symbols_finish_on_the_host_when_the_device_path_fails(oracle_mod):
+    """RDK_HIP_MAX_SCRATCH_BYTES caps pinned staging and device scratch.  Under a 1 MiB cap a
+    just-under-1 MiB crc32c() gets its pinned staging but not its device staging (two failed
+    attempts, then the host finishes from the staged bytes); a 3 MiB one gets neither.  The
+    checksums must be right, the calls counted, and the process must live on."""
+    code = textwrap.dedent("""
+        import sys
+        sys.path.insert(0, %r)
+        import librdkafka_amd as L, oracle
+        from librdkafka_amd import workload as W
+        L.init(0)
+        small = W.gen_json(4000, 3)
+        assert L.crc32c(0, small) == oracle.crc32c(0, small) and L.dropin_host_crcs() == 0
+        a = W.gen_json((1 << 20) - 10, 1)
+        assert L.crc32c(7, a) == oracle.crc32c(7, a)
+        assert L.dropin_host_crcs() == 1
+        b = W.gen_json(3 << 20, 2)
+        assert L.crc32c(0, b) == oracle.crc32c(0, b)
+        assert L.rd_slice_crc32c([b[:61], b[61:]]) == oracle.crc32c(0, b)
+        import zlib
+        assert L.rd_slice_crc32([b[:1000], b[1000:]]) == zlib.crc32(b)
+        assert L.dropin_host_crcs() == 4
+        assert L.crc32c(0, small) == oracle.crc32c(0, small) and L.dropin_host_crcs() == 4
+        print("survived")
+    """ % ROOT)
+    env = dict(os.environ, RDK_HIP_MAX_SCRATCH_BYTES=str(1 << 20))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 0 and "survived" in r.stdout, (r.returncode, r.stdout, r.stderr[-2000:])
+    assert "computed on the host" in r.stderr
+
+
+def _frame(bd, blocks):
+    """LZ4F frame, independent blocks, no checksums; blocks = [(raw?, payload)]."""
+    import xxhash
+    flg = 0x60
+    hc = (xxhash.xxh32(bytes([flg, bd])).intdigest() >> 8) & 0xFF
+    out = bytes([0x04, 0x22, 0x4D, 0x18, flg, bd, hc])
+    for raw, p in blocks:
+        out += struct.pack("<I", len(p) | (0x80000000 if raw else 0)) + p
+    return out + bytes(4)
+
+
+def test_decompress_many_short_blocks_of_a_4MiB_class(engine, oracle_mod):
+    """A small frame of hundreds of short blocks declaring 4 MiB blocks: the block table
+    alone must not size gigabytes of staging (it is sized from what the blocks can yield),
+    and the payload must still be the reference's."""
+    blocks, want = [], b""
+    for i in range(700):
+        if i % 3 == 0:
+            p = W.gen_json(40 + i % 50, i)
+            blocks.append((True, p))
+            want += p
+        else:  # one literal run: token (len << 4) + bytes
+            p = W.gen_json(1 + i % 14, 1000 + i)
+            blocks.append((False, bytes([len(p) << 4]) + p))
+            want += p
+    fr = _frame(0x70, blocks)
+    oerr, oout = oracle_mod.rdk_lz4_decompress(fr)
+    assert oerr == 0 and oout == want
+    assert engine.rd_kafka_lz4_decompress(1, 0, fr) == (0, want)
+    # and a mixed one: a full-size first block, then short ones (in-place layout would need
+    # its slots; the tight size still holds everything in stream order)
+    big = W.gen_json(65536, 9)
+    err, full = engine.rd_kafka_lz4_compress(1, 0, big)
+    assert err == 0
+    first = full[7:-4]  # the one block of that frame, with its size word
+    fr2 = full[:7] + first + b"".join(struct.pack("<I", len(p) | 0x80000000) + p
+                                      for p in (b"abc", b"defgh", b"i")) + bytes(4)
+    assert engine.rd_kafka_lz4_decompress(1, 0, fr2) == oracle_mod.rdk_lz4_decompress(fr2) == \
+        (0, big + b"abcdefghi")
+
+
+def test_snappy_dropins_around_the_staging_growth_sizes(engine, oracle_mod):
+    """A thread's first snappy compress of ~1 MiB, then 2 MiB: the pinned staging is sized
+    for the stream before the input is gathered into it, so growing it must not lose the
+    input (fresh thread: a fresh context with no staging yet)."""
+    res = {}
+
+    def run():
+        for n, seed in ((1_000_000, 11), (2_000_000, 12), (1 << 20, 13)):
+            data = W.gen_json(n, seed)
+            err, stream = engine.rd_kafka_snappy_compress_iov([data[:300000], data[300000:]])
+            res[n] = (err, stream == oracle_mod.snappy_compress(data),
+                      engine.rd_kafka_snappy_decompress(stream) == (0, data))
+
+    t = threading.Thread(target=run)
+    t.start()
+    t.join()
+    assert res == {n: (0, True, True) for n in (1_000_000, 2_000_000, 1 << 20)}, res

@@ -126,3 +126,90 @@ def test_messages_to_batches_to_rows(engine, oracle_mod, mode):
                     p = int(do[i]) + int(r[f + "_off"][g])
                     o = int(m[f + "_off"][g])
                     assert bytes(decoded[p:p + want_len]) == bytes(arena[o:o + want_len])
+
+
+def test_perf_tool_messages_through_writer_and_reader(engine, oracle_mod):
+    """The workload of `rdkafka_performance -P -s 100 -z lz4` (examples/rdkafka_performance.c:798,
+    :1318-1325): 100-byte messages of the repeated pattern, no key, cut into MessageSets by
+    write_msgq's rule (batch.num.messages 10000, message.max.bytes 1000000,
+    rdkafka_msgset_writer.c:859-863).  Every finished batch must equal the oracle's writer +
+    the reference-identical LZ4F frame + CRC32C byte for byte, and the reader side must hand
+    back the messages."""
+    import torch
+    m = W.gen_perf_messages(30000)
+    spec = W.perf_batches(m)
+    assert len(spec) == 4 and spec[0][1] > 9000 and sum(c for _, c in spec) == 30000
+    n = len(spec)
+    b = np.zeros(n, dtype=E.V2_BATCH_DTYPE)
+    for i, (first, cnt) in enumerate(spec):
+        b[i] = (first, cnt, -1, -1, -1, 0)
+    d = _dev(m)
+    sets, offs, sizes, _ = E.msgset_v2_build(d, b, crc=False)
+    rec_offs, rec_lens = offs + 61, sizes - 61
+    caps = [(61 + E.lz4f_compress_bound(int(x)) + 255) // 256 * 256 for x in rec_lens.cpu().numpy()]
+    out_offs = torch.tensor(np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64), device="cuda")
+    out_caps = torch.tensor(np.asarray(caps, np.int32), device="cuda")
+    out = torch.zeros(int(sum(caps)) + 256, dtype=torch.uint8, device="cuda")
+    flens, blens, crcs = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    E.msgset_v2_finalize(sets, rec_offs, rec_lens, out, out_offs, out_caps, flens, blens, crcs,
+                         mode=E.PRODUCER_EXACT)
+    host = bytes(out.cpu().numpy())
+    oo, bl = out_offs.cpu().numpy(), blens.cpu().numpy()
+    got_crcs = crcs.cpu().numpy().view(np.uint32)
+    for i, (first, cnt) in enumerate(spec):
+        want_set = oracle_mod.msgset_v2_write(m, first, cnt, -1, -1, -1, 0)
+        assert len(want_set) <= 1000000 + 61
+        err, frame = oracle_mod.rdk_lz4_compress(want_set[61:])
+        assert err == 0 and len(frame) < len(want_set) - 61
+        got = host[oo[i]:oo[i] + bl[i]]
+        assert got[61:] == frame, i
+        hdr = bytearray(want_set[:61])
+        hdr[8:12] = (len(got) - 12).to_bytes(4, "big")
+        hdr[21:23] = (int.from_bytes(hdr[21:23], "big") | 3).to_bytes(2, "big")
+        crc = oracle_mod.crc32c(0, bytes(hdr[21:]) + frame)
+        hdr[17:21] = crc.to_bytes(4, "big")
+        assert got[:61] == bytes(hdr), i
+        assert int(got_crcs[i]) == crc
+    # the throughput compressor on the same MessageSets: decodable by the reference, ratio in bound
+    out2 = torch.zeros_like(out)
+    fl2, bl2, cr2 = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    E.msgset_v2_finalize(sets, rec_offs, rec_lens, out2, out_offs, out_caps, fl2, bl2, cr2,
+                         mode=E.PRODUCER_FAST)
+    host2 = bytes(out2.cpu().numpy())
+    for i, (first, cnt) in enumerate(spec):
+        want_set = oracle_mod.msgset_v2_write(m, first, cnt, -1, -1, -1, 0)
+        got = host2[oo[i]:oo[i] + int(bl2[i])]
+        assert int.from_bytes(got[17:21], "big") == oracle_mod.crc32c(0, got[21:])
+        dec_ref = (oracle_mod.ref_rdk_lz4_decompress(got[61:], max_msg_size=1 << 30)[:2]
+                   if oracle_mod.ref_available() else oracle_mod.rdk_lz4_decompress(got[61:]))
+        assert dec_ref == (0, want_set[61:]), i
+        assert len(got) - 61 <= 1.05 * int(flens[i]), (i, len(got) - 61, int(flens[i]))
+    # ---- reader: check.crcs, decompress, record index
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    E.msgset_v2_crc(out, out_offs, out_caps, st, E.V2_CRC_VERIFY)
+    assert int(st.abs().sum()) == 0
+    rl = rec_lens.cpu().numpy().astype(np.int64)
+    dslot = (rl + 255) // 256 * 256
+    doffs = torch.tensor(np.concatenate([[0], np.cumsum(dslot)[:-1]]).astype(np.int64), device="cuda")
+    dcaps = torch.tensor(dslot.astype(np.int32), device="cuda")
+    dec = torch.zeros(int(dslot.sum()) + 256, dtype=torch.uint8, device="cuda")
+    dl, ds = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(2))
+    E.lz4f_decompress_batch(out, out_offs + 61, flens, dec, doffs, dcaps, dl, ds)
+    assert int(ds.abs().sum()) == 0 and bool((dl == rec_lens).all())
+    row_offs = torch.tensor(np.asarray([s[0] for s in spec], np.int64), device="cuda")
+    row_caps = torch.tensor(np.asarray([s[1] for s in spec], np.int32), device="cuda")
+    rows = {k: torch.zeros(30000, dtype=getattr(torch, t), device="cuda") for k, t in E.V2_ROW_FIELDS}
+    cnt = torch.zeros(n, dtype=torch.int32, device="cuda")
+    E.msgset_v2_index(out, out_offs, dec, doffs, dl, row_offs, row_caps, rows, cnt)
+    assert cnt.cpu().tolist() == [c for _, c in spec]
+    r = {k: v.cpu().numpy() for k, v in rows.items()}
+    assert (r["timestamp"] == m["ts"]).all() and (r["val_len"] == 100).all() and (r["key_len"] == -1).all()
+    want_off = np.concatenate([np.arange(c) for _, c in spec])
+    assert (r["offset"] == want_off).all()
+    decoded = dec.cpu().numpy()
+    do = doffs.cpu().numpy()
+    value = bytes(m["arena"][:100])
+    for i, (first, c) in enumerate(spec):
+        for j in (0, 1, c // 2, c - 1):
+            p = int(do[i]) + int(r["val_off"][first + j])
+            assert bytes(decoded[p:p + 100]) == value

@@ -34,7 +34,14 @@ def test_thread_context_is_released_at_thread_exit(engine, oracle_mod):
         t = threading.Thread(target=broker_thread)
         t.start()
         t.join()
-    c1, d1 = engine.ctx_counts()
+    # join() returns when the Python function has returned; the OS thread runs its
+    # thread-exit destructors a moment later
+    import time
+    for _ in range(200):
+        c1, d1 = engine.ctx_counts()
+        if d1 - d0 == 6:
+            break
+        time.sleep(0.01)
     assert c1 - c0 == 6 and d1 - d0 == 6, (c0, d0, c1, d1)
     for i in range(6):
         assert got[2 * i] == want

@@ -252,6 +252,19 @@ int rdk_hip_lz4f_compress_fast(const void *d_in, const uint64_t *d_in_offs,
                                const uint64_t *d_out_offs, uint32_t *d_out_lens,
                                uint32_t n, void *stream);
 
+/* The same contract as rdk_hip_lz4f_compress_fast on another engine: one 1024-thread
+ * workgroup per 64 KB block with the block's source, the hash table and the output
+ * staging in LDS, so a block's bytes are read from memory once and its output leaves in
+ * aligned 16-byte stores (the one-wavefront-per-block engine behind _fast gathers its
+ * candidates from memory).  Its output is defined by a sequential model
+ * (tests/sim/lz4_units_sim.cpp) that it reproduces byte for byte.  No counterpart in the
+ * reference.  RDK_HIP_LZ4_FAST_ENGINE=units in the environment makes _fast and the
+ * producer's FAST mode run this engine. */
+int rdk_hip_lz4f_compress_units(const void *d_in, const uint64_t *d_in_offs,
+                                const uint32_t *d_in_lens, void *d_out,
+                                const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                                uint32_t n, void *stream);
+
 /* LZ4F decompression of n independent frames (rd_kafka_lz4_decompress
  * semantics per frame, proper HC).  Frame i decodes into
  * d_out + d_out_offs[i] with capacity d_out_caps[i]; d_out_lens[i] gets the

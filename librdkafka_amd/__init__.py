@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "rd_kafka_snappy_uncompressed_length", "rd_kafka_snappy_compress_iov",
     "rd_kafka_snappy_compress", "rd_kafka_snappy_uncompress", "rd_kafka_snappy_java_uncompress",
     "rdk_hip_snappy_dropin_calls", "rdk_hip_dropin_host_crcs", "rdk_hip_ctx_counts",
+    "rdk_hip_lz4f_compress_units",
 )
 
 
@@ -113,6 +114,8 @@ def lib():
         L.rdk_hip_lz4f_compress.argtypes = [vp, vp, vp, vp, vp, vp, u32, i32, vp]
         L.rdk_hip_lz4f_compress_fast.restype = i32
         L.rdk_hip_lz4f_compress_fast.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp]
+        L.rdk_hip_lz4f_compress_units.restype = i32
+        L.rdk_hip_lz4f_compress_units.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp]
         L.rdk_hip_lz4f_decompress.restype = i32
         L.rdk_hip_lz4f_decompress.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
         L.rdk_hip_lz4f_decompress_noalloc.restype = i32
@@ -382,6 +385,14 @@ def lz4f_compress_fast_batch(src, in_offs, in_lens, dst, out_offs, out_lens, str
     _check(lib().rdk_hip_lz4f_compress_fast(_ptr(src), _ptr(in_offs), _ptr(in_lens), _ptr(dst),
                                             _ptr(out_offs), _ptr(out_lens), int(in_offs.numel()),
                                             _stream(stream)), "lz4f_compress_fast")
+
+
+def lz4f_compress_units_batch(src, in_offs, in_lens, dst, out_offs, out_lens, stream=None):
+    """rdk_hip_lz4f_compress_units: the throughput compressor's workgroup-per-block engine
+    (csrc/lz4_encode_units.hip), same contract as lz4f_compress_fast_batch."""
+    _check(lib().rdk_hip_lz4f_compress_units(_ptr(src), _ptr(in_offs), _ptr(in_lens), _ptr(dst),
+                                             _ptr(out_offs), _ptr(out_lens), int(in_offs.numel()),
+                                             _stream(stream)), "lz4f_compress_units")
 
 
 def lz4f_decompress_batch(src, in_offs, in_lens, dst, out_offs, out_caps, out_lens, status,

@@ -996,7 +996,11 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
       // ---- calc_crc_v2 (:1229-1246) over [21, 61 + payload) without re-reading the frame:
       // header bytes and LZ4F header through the byte table, then one term per block
       uint32_t crc;
-      if (compressed && nb <= 64u) {
+      if (!fuse.block_crc) {
+        // no block registers (the unit engine): the caller runs the batched CRC32C pass
+        // over the finished batches behind this kernel
+        crc = 0;
+      } else if (compressed && nb <= 64u) {
         if (uint32_t(t) < nb) {
           uint32_t after = 4u;                            // the end mark
           for (uint32_t j = uint32_t(t) + 1u; j < nb; ++j) after += 4u + s_sz[j];
@@ -1080,6 +1084,10 @@ int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
 int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, int level, hipStream_t s);
+int lz4f_compress_units_device(const uint8_t *d_in, const uint64_t *d_in_offs,
+                               const uint32_t *d_in_lens, uint8_t *d_out,
+                               const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
+                               hipStream_t s, const FuseCrc *fuse);
 
 }  // namespace rdk
 
@@ -1119,4 +1127,18 @@ RDK_API int rdk_hip_lz4f_compress_fast(const void *d_in, const uint64_t *d_in_of
   return lz4f_compress_fast_device(static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
                                    static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n,
                                    static_cast<hipStream_t>(stream), nullptr);
+}
+
+RDK_API int rdk_hip_lz4f_compress_units(const void *d_in, const uint64_t *d_in_offs,
+                                        const uint32_t *d_in_lens, void *d_out,
+                                        const uint64_t *d_out_offs, uint32_t *d_out_lens,
+                                        uint32_t n, void *stream) {
+  Ctx *c = ctx();
+  if (!c) return RDK_HIP_E_NODEV;
+  if (!n) return RDK_HIP_OK;
+  if (!d_in || !d_in_offs || !d_in_lens || !d_out || !d_out_offs || !d_out_lens)
+    return set_error(RDK_HIP_E_INVAL, "null pointer");
+  return lz4f_compress_units_device(static_cast<const uint8_t *>(d_in), d_in_offs, d_in_lens,
+                                    static_cast<uint8_t *>(d_out), d_out_offs, d_out_lens, n,
+                                    static_cast<hipStream_t>(stream), nullptr);
 }

@@ -30,6 +30,8 @@
 // reference's by tests/test_gpu_lz4.py (north_star: within 5 %).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "crc_wave.h"
 #include "lz4_device.h"
@@ -370,11 +372,30 @@ __global__ __launch_bounds__(64) void lz4_fast_blocks_kernel(
 
 }  // namespace
 
+int lz4f_compress_units_device(const uint8_t *d_in, const uint64_t *d_in_offs,
+                               const uint32_t *d_in_lens, uint8_t *d_out,
+                               const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
+                               hipStream_t s, const FuseCrc *fuse);
+
+// RDK_HIP_LZ4_FAST_ENGINE=units makes the throughput entry points (and the producer's FAST
+// mode) run the workgroup-per-block engine of lz4_encode_units.hip instead of this file's
+// one-wavefront-per-block engine (A/B runs; rdk_hip_lz4f_compress_units always runs it).
+bool lz4f_fast_engine_is_units() {
+  static const bool units = [] {
+    const char *e = getenv("RDK_HIP_LZ4_FAST_ENGINE");
+    return e && e[0] == 'u';
+  }();
+  return units;
+}
+
 int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
                               const uint32_t *d_in_lens, uint8_t *d_out,
                               const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
                               hipStream_t s, const FuseCrc *fuse) {
   if (!n) return 0;
+  if (lz4f_fast_engine_is_units())
+    return lz4f_compress_units_device(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n,
+                                      s, fuse);
   const uint64_t items = uint64_t(n) * kFastMaxItems;
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
   hipLaunchKernelGGL(lz4_fast_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,

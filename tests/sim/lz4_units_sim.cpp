@@ -8,7 +8,7 @@
 // against the reference decoder and the reference's compression ratio without a GPU.
 //
 //   1. Candidates, in position order, 64 positions at a time: every position i <= n-12 is
-//      hashed with LZ4_hash4 (lz4.c:631, 12-bit table) and takes as its candidate the
+//      hashed with LZ4_hash4 (lz4.c:631, 13-bit table as LZ4_compress_generic's byU16, lz4.c:633) and takes as its candidate the
 //      table's entry as it stood before its group of 64; then the whole group is entered
 //      (the highest position of a group wins an entry).
 //   2. The block is cut into units of `unit_windows` x 64 positions.  A unit is parsed
@@ -31,7 +31,7 @@
 #include <vector>
 
 namespace {
-constexpr int kMinMatch = 4, kLastLiterals = 5, kMFLimit = 12, kHashLog = 12;
+constexpr int kMinMatch = 4, kLastLiterals = 5, kMFLimit = 12, kHashLog = 13;
 
 inline uint32_t rd32(const uint8_t *p) {
   uint32_t v;

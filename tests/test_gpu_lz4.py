@@ -283,7 +283,7 @@ def test_batch_scale_roundtrip_property(engine):
 
 
 # ------------------------------------------------ throughput-mode compressor
-def _fast_compress(engine, inputs):
+def _fast_compress(engine, inputs, units=False):
     import torch
     hbuf, hoffs = _pack(inputs)
     d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
@@ -295,7 +295,8 @@ def _fast_compress(engine, inputs):
                         device="cuda")
     out_offs = torch.tensor(ooffs, dtype=torch.int64, device="cuda")
     out_lens = torch.zeros(len(inputs), dtype=torch.int32, device="cuda")
-    engine.lz4f_compress_fast_batch(d_in, in_offs, in_lens, d_out, out_offs, out_lens)
+    comp = engine.lz4f_compress_units_batch if units else engine.lz4f_compress_fast_batch
+    comp(d_in, in_offs, in_lens, d_out, out_offs, out_lens)
     host_out = bytes(d_out.cpu().numpy())
     flens = out_lens.cpu().numpy()
     return [host_out[ooffs[i]:ooffs[i] + flens[i]] for i in range(len(inputs))]
@@ -323,14 +324,15 @@ def _fast_inputs(seed, count):
     return out
 
 
-def test_fast_compress_decodes_with_reference(engine, oracle_mod):
+@pytest.mark.parametrize("units", [False, True], ids=["wave-engine", "units-engine"])
+def test_fast_compress_decodes_with_reference(engine, oracle_mod, units):
     """Every throughput-mode frame decodes to its input with the reference's
     own decoder (oracle/_ref build of lz4frame.c via rd_kafka_lz4_decompress's
     loop when present here; the pinned restatement on the GPU box) and with
     the GPU decoder; frame structure is the reference's (header, 64 KiB
     independent blocks, raw fallback, end mark)."""
     inputs = _fast_inputs(41, 30)
-    frames = _fast_compress(engine, inputs)
+    frames = _fast_compress(engine, inputs, units)
     use_ref = oracle_mod.ref_available()
     for i, (b, fr) in enumerate(zip(inputs, frames)):
         assert fr[:7] == bytes([0x04, 0x22, 0x4D, 0x18, 0x60, 0x40, 0x82]), i
@@ -344,7 +346,8 @@ def test_fast_compress_decodes_with_reference(engine, oracle_mod):
         assert len(fr) <= engine.lz4f_compress_bound(len(b)), i
 
 
-def test_fast_compress_ratio_within_5pct(engine, oracle_mod):
+@pytest.mark.parametrize("units", [False, True], ids=["wave-engine", "units-engine"])
+def test_fast_compress_ratio_within_5pct(engine, oracle_mod, units):
     """north_star: compression ratio within 5 % of the reference's CPU lz4 on
     the same input (JSON records of configs[2], text-like and repetitive)."""
     rnd = random.Random(43)
@@ -353,16 +356,35 @@ def test_fast_compress_ratio_within_5pct(engine, oracle_mod):
     text = b" ".join(rnd.choice(words) for _ in range(300000))[:1 << 20]
     inputs = [W.gen_json(1 << 20, 42), W.gen_json(65536, 7), W.gen_json(1 << 20, 5), text,
               (rnd.randbytes(3000) * 400)[:1 << 20]]
-    frames = _fast_compress(engine, inputs)
+    frames = _fast_compress(engine, inputs, units)
     for i, (b, fr) in enumerate(zip(inputs, frames)):
         ref = oracle_mod.rdk_lz4_compress(b)[1]
         r_gpu, r_ref = len(b) / len(fr), len(b) / len(ref)
         assert r_gpu >= 0.95 * r_ref, (i, r_gpu, r_ref)
 
 
-def test_fast_compress_deterministic(engine):
+def test_units_engine_equals_the_sequential_model(engine):
+    """The workgroup-per-block engine's output is defined by tests/sim/lz4_units_sim.cpp (candidates
+    in position order, units parsed on their own, stitched in order): the kernel's frames
+    must be that model's frames byte for byte, on every input family and edge size."""
+    import units_model
+    rnd = random.Random(45)
+    inputs = _fast_inputs(45, 20)
+    inputs += [W.gen_json(n, n) for n in (895, 896, 897, 13439, 13440, 13441, 26880, 65536 + 896)]
+    inputs += [bytes(70000), (rnd.randbytes(3000) * 400)[:1 << 20], (rnd.randbytes(70) * 3000)[:200000]]
+    m = W.gen_perf_messages(3000)
+    inputs.append(W.PERF_PATTERN * 4000)
+    del m
+    frames = _fast_compress(engine, inputs, units=True)
+    for i, (b, fr) in enumerate(zip(inputs, frames)):
+        want = units_model.frame(b)
+        assert fr == want, (i, len(b), len(fr), len(want))
+
+
+@pytest.mark.parametrize("units", [False, True], ids=["wave-engine", "units-engine"])
+def test_fast_compress_deterministic(engine, units):
     inputs = _fast_inputs(44, 8)
-    assert _fast_compress(engine, inputs) == _fast_compress(engine, inputs)
+    assert _fast_compress(engine, inputs, units) == _fast_compress(engine, inputs, units)
 
 
 def test_batch_compress_window_engine_inputs(engine, oracle_mod):

@@ -213,3 +213,57 @@ def test_perf_tool_messages_through_writer_and_reader(engine, oracle_mod):
         for j in (0, 1, c // 2, c - 1):
             p = int(do[i]) + int(r["val_off"][first + j])
             assert bytes(decoded[p:p + 100]) == value
+
+
+def test_finalize_fast_on_the_units_engine(oracle_mod):
+    """RDK_HIP_LZ4_FAST_ENGINE=units: rdk_hip_msgset_v2_finalize's FAST mode on the
+    workgroup-per-block compressor, whose CRC32C comes from the batched CRC pass over the
+    finished batches instead of the compress epilogue.  Own process: the engine choice is read
+    once from the environment.  Every batch: header fields, CRC against the oracle, frame
+    decoded by the reference decoder."""
+    import os
+    import subprocess
+    import sys
+    import textwrap
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent("""
+        import sys
+        sys.path.insert(0, %r)
+        import numpy as np, torch
+        import librdkafka_amd as E, oracle
+        from librdkafka_amd import workload as W
+        E.init(0)
+        recs = [W.gen_json(n, 3 + i) for i, n in enumerate((1 << 20, 70000, 13, 5, 300000))] + \\
+               [bytes(np.random.default_rng(1).integers(0, 256, 90000, dtype=np.uint8))]
+        n = len(recs)
+        stride = (61 + max(map(len, recs)) + 255) // 256 * 256
+        src = torch.zeros(n * stride + 256, dtype=torch.uint8)
+        for i, r in enumerate(recs):
+            src[i * stride:i * stride + 61] = torch.frombuffer(bytearray(W.v2_header(i, 61 + len(r))), dtype=torch.uint8)
+            src[i * stride + 61:i * stride + 61 + len(r)] = torch.frombuffer(bytearray(r), dtype=torch.uint8)
+        src = src.cuda()
+        rec_offs = torch.arange(n, dtype=torch.int64, device="cuda") * stride + 61
+        rec_lens = torch.tensor([len(r) for r in recs], dtype=torch.int32, device="cuda")
+        cap = (61 + E.lz4f_compress_bound(max(map(len, recs))) + 255) // 256 * 256
+        out = torch.zeros(n * cap + 256, dtype=torch.uint8, device="cuda")
+        out_offs = torch.arange(n, dtype=torch.int64, device="cuda") * cap
+        out_caps = torch.full((n,), cap, dtype=torch.int32, device="cuda")
+        fl, bl, cr = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+        E.msgset_v2_finalize(src, rec_offs, rec_lens, out, out_offs, out_caps, fl, bl, cr, mode=E.PRODUCER_FAST)
+        host = bytes(out.cpu().numpy())
+        crcs = cr.cpu().numpy().view(np.uint32)
+        for i, r in enumerate(recs):
+            got = host[i * cap:i * cap + int(bl[i])]
+            codec = int.from_bytes(got[21:23], "big") & 7
+            assert int.from_bytes(got[8:12], "big") == len(got) - 12, i
+            assert int.from_bytes(got[17:21], "big") == oracle.crc32c(0, got[21:]) == int(crcs[i]), i
+            if codec == 3:
+                assert oracle.rdk_lz4_decompress(got[61:]) == (0, r), i
+            else:
+                assert codec == 0 and got[61:] == r, i
+        assert (int.from_bytes(host[21:23], "big") & 7) == 3 and (int.from_bytes(host[5 * cap + 21:5 * cap + 23], "big") & 7) == 0
+        print("ok")
+    """ % root)
+    env = dict(os.environ, RDK_HIP_LZ4_FAST_ENGINE="units")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.returncode, r.stdout, r.stderr[-3000:])

@@ -47,13 +47,19 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
+SIMDS = 1024                   # 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9               # MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
 def profile_summary(leg: str, alg_bytes: int, kernel_ms: float):
-    """(traffic_bytes, note) from profiles/r02/<leg>.json -- the rocprofv3 summary of this leg
-    (scripts/profile_r2.sh) -- only when it was taken from the same kernel sources and the
-    same algorithmic bytes; its kernel-trace average must agree with the HIP-event time."""
+    """(traffic_bytes, note) from profiles/r03/<leg>.json -- the rocprofv3 summary of this leg
+    (scripts/profile_r3.sh) -- only when it was taken from the same kernel sources and the
+    same algorithmic bytes; its kernel-trace average must agree with the HIP-event time.
+    With an SQ_INSTS_VALU pass in the summary the note carries `issue`: the vector
+    instructions per launch and the time the chip needs just to issue them (one wave64
+    vector instruction per SIMD per 4 cycles), the ceiling that binds the LZ4 / snappy legs
+    long before HBM does."""
     path = os.path.join(PROFILE_DIR, leg + ".json")
     try:
         with open(path) as f:
@@ -70,6 +76,16 @@ def profile_summary(leg: str, alg_bytes: int, kernel_ms: float):
         return None, note
     if p.get("avg_ns") and kernel_ms:
         note["profile_vs_events"] = round(p["avg_ns"] / 1e6 / kernel_ms, 4)
+    if p.get("valu_insts"):
+        floor_ms = p["valu_insts"] * 4.0 / (SIMDS * CLOCK_HZ) * 1e3
+        note["issue"] = {"valu_insts_per_launch": int(p["valu_insts"]),
+                         "valu_per_alg_byte": round(p["valu_insts"] * 64.0 / alg_bytes, 3),
+                         "lane_ops_per_alg_byte": round(p["valu_insts"] * 64.0 / alg_bytes, 3),
+                         "issue_floor_ms": round(floor_ms, 4),
+                         "frac_of_issue_ceiling": round(floor_ms / kernel_ms, 4) if kernel_ms else None,
+                         "note": "SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz)"}
+        note["issue"].pop("lane_ops_per_alg_byte")
+        note["issue"]["valu_wave_insts_per_64_alg_bytes"] = note["issue"].pop("valu_per_alg_byte")
     return (int(p["traffic_bytes"]) if "traffic_bytes" in p else None), note
 
 
@@ -192,18 +208,37 @@ def _timed(fn, steps, warmup, world):
     return wall * 1e3 / steps, ev0.elapsed_time(ev1) / steps
 
 
-def json_batches(n, size=JSON_BATCH, seed=42):
-    """n device-resident 1 MiB batches of JSON-like records (8 distinct MiB
-    rotated: generation cost stays off the GPU clock, contents stay realistic)."""
+DISTINCT_BYTES = 8 << 20     # distinct JSON bytes behind every leg's batches (rotated)
+
+
+def _json_base(size, seed):
+    """(host bytes, device tensor [distinct, size]) of distinct = 8 MiB / size batches."""
     import torch
     import librdkafka_amd as L
-    distinct = 8
+    distinct = max(8, DISTINCT_BYTES // size)
     host = L.gen_json(size * distinct, seed)
-    base = torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda()
+    base = torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda().view(distinct, size)
+    return host, base, distinct
+
+
+def json_record_count(host, size, n):
+    """JSON records (lines) that end in n batches of `size` bytes cut from `host` in rotation:
+    the messages the batches carry."""
+    distinct = len(host) // size
+    per = [host[j * size:(j + 1) * size].count(b"\n") for j in range(distinct)]
+    return sum(per) * (n // distinct) + sum(per[:n % distinct])
+
+
+def json_batches(n, size=JSON_BATCH, seed=42):
+    """n device-resident batches of `size` bytes of JSON-like records (8 distinct MiB
+    rotated: generation cost stays off the GPU clock, contents stay realistic)."""
+    import torch
+    host, base, distinct = _json_base(size, seed)
     buf = torch.empty(n * size + 256, dtype=torch.uint8, device="cuda")
-    for i in range(n):
-        j = i % distinct
-        buf[i * size:(i + 1) * size] = base[j * size:(j + 1) * size]
+    idx = torch.arange(n, device="cuda") % distinct
+    for lo in range(0, n, 4096):  # (in slices: the gather's temporary stays small)
+        hi = min(n, lo + 4096)
+        buf[lo * size:hi * size].view(hi - lo, size).copy_(base[idx[lo:hi]])
     offs = torch.arange(n, dtype=torch.int64, device="cuda") * size
     lens = torch.full((n,), size, dtype=torch.int32, device="cuda")
     return buf, offs, lens
@@ -211,42 +246,39 @@ def json_batches(n, size=JSON_BATCH, seed=42):
 
 def json_msgsets(n, size=JSON_BATCH, seed=42):
     """n device-resident MessageSets as the writer leaves them before finalize: a 61-byte v2
-    header directly followed by `size` bytes of JSON records (8 distinct MiB rotated)."""
-    import numpy as np
+    header directly followed by `size` bytes of JSON records (8 distinct MiB rotated).
+    Returns (buffer, record offsets, record lengths, records carried)."""
     import torch
-    import librdkafka_amd as L
     from librdkafka_amd import workload as W
-    distinct = 8
-    host = L.gen_json(size * distinct, seed)
-    base = torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda()
+    host, base, distinct = _json_base(size, seed)
     stride = (61 + size + 255) // 256 * 256
     buf = torch.zeros(n * stride + 256, dtype=torch.uint8, device="cuda")
     hdrs = torch.frombuffer(bytearray(b"".join(W.v2_header(i, 61 + size) for i in range(n))),
                             dtype=torch.uint8).cuda().view(n, 61)
     v = buf[:n * stride].view(n, stride)
     v[:, :61] = hdrs
-    for i in range(n):
-        j = i % distinct
-        v[i, 61:61 + size] = base[j * size:(j + 1) * size]
+    idx = torch.arange(n, device="cuda") % distinct
+    for lo in range(0, n, 4096):
+        hi = min(n, lo + 4096)
+        v[lo:hi, 61:61 + size] = base[idx[lo:hi]]
     rec_offs = torch.arange(n, dtype=torch.int64, device="cuda") * stride + 61
     rec_lens = torch.full((n,), size, dtype=torch.int32, device="cuda")
-    del np
-    return buf, rec_offs, rec_lens
+    return buf, rec_offs, rec_lens, json_record_count(host, size, n)
 
 
-def bench_finalize(args, rank, world, n=None, mode=0):
+def bench_finalize(args, rank, world, n=None, mode=0, size=JSON_BATCH):
     """The headline step: rdk_hip_msgset_v2_finalize (LZ4F compress + v2 header finalize +
-    CRC32C finalize, rdkafka_msgset_writer.c:1335) over n device-resident 1 MiB MessageSets.
-    mode 0 = frames byte-identical to rd_kafka_lz4_compress, 1 = the throughput compressor.
-    The step is two kernels (block compress with the CRC epilogue, frame assembly with header
-    finalize and CRC combine); its HIP-event time feeds the roofline.  The finished batches
+    CRC32C finalize, rdkafka_msgset_writer.c:1335) over n device-resident MessageSets of
+    `size` record bytes.  mode 1 = the throughput compressor (reference-decodable frames,
+    ratio within 5 % of the reference's: north_star's bar), 0 = frames byte-identical to
+    rd_kafka_lz4_compress.  Its HIP-event time feeds the roofline.  The finished batches
     are checked on the device: CRC VERIFY all zero, every frame decompressed by the engine
     equals its records."""
     import torch
     import librdkafka_amd as L
     n = n or args.partitions
-    src, rec_offs, rec_lens = json_msgsets(n, seed=42 + rank)
-    cap = (61 + L.lz4f_compress_bound(JSON_BATCH) + 255) // 256 * 256
+    src, rec_offs, rec_lens, nrecords = json_msgsets(n, size, seed=42 + rank)
+    cap = (61 + L.lz4f_compress_bound(size) + 255) // 256 * 256
     dst = torch.empty(n * cap + 256, dtype=torch.uint8, device="cuda")
     out_offs = torch.arange(n, dtype=torch.int64, device="cuda") * cap
     out_caps = torch.full((n,), cap, dtype=torch.int32, device="cuda")
@@ -263,48 +295,50 @@ def bench_finalize(args, rank, world, n=None, mode=0):
     L.msgset_v2_crc(dst, out_offs, out_caps, st, L.V2_CRC_VERIFY)
     if int(st.abs().sum()):
         raise SystemExit(f"rank {rank}: CRC verify failures in the finished batches")
-    dec = torch.empty(n * JSON_BATCH + 256, dtype=torch.uint8, device="cuda")
-    doffs = torch.arange(n, dtype=torch.int64, device="cuda") * JSON_BATCH
-    dcaps = torch.full((n,), JSON_BATCH, dtype=torch.int32, device="cuda")
+    dslot = (size + 255) // 256 * 256
+    dec = torch.empty(n * dslot + 256, dtype=torch.uint8, device="cuda")
+    doffs = torch.arange(n, dtype=torch.int64, device="cuda") * dslot
+    dcaps = torch.full((n,), dslot, dtype=torch.int32, device="cuda")
     dl = torch.zeros(n, dtype=torch.int32, device="cuda")
     L.lz4f_decompress_batch(dst, frame_offs, flens, dec, doffs, dcaps, dl, st)
-    stride = (61 + JSON_BATCH + 255) // 256 * 256
-    recs = src[:n * stride].view(n, stride)[:, 61:61 + JSON_BATCH]
-    if int(st.abs().sum()) or not bool((dl == JSON_BATCH).all()) or \
-            not torch.equal(dec[:n * JSON_BATCH].view(n, JSON_BATCH), recs):
+    stride = (61 + size + 255) // 256 * 256
+    recs = src[:n * stride].view(n, stride)[:, 61:61 + size]
+    if int(st.abs().sum()) or not bool((dl == size).all()) or \
+            not torch.equal(dec[:n * dslot].view(n, dslot)[:, :size], recs):
         raise SystemExit(f"rank {rank}: finished frames do not decompress to their records")
     if not bool((blens == flens + 61).all()):
         raise SystemExit(f"rank {rank}: a JSON batch was left uncompressed")
     clen = int(flens.to(torch.int64).sum())
-    nbytes = n * JSON_BATCH
-    return {"ms": ms, "kernel_ms": kms, "bytes": nbytes, "records": n,
-            # step: records read + frame written, header read + written (the CRC comes out
-            # of the compress epilogue: the frame is not read again)
+    nbytes = n * size
+    return {"ms": ms, "kernel_ms": kms, "bytes": nbytes, "records": n, "messages": nrecords,
+            # step: records read + frame written, header read + written
             "alg_bytes": nbytes + clen + 2 * 61 * n, "ratio": nbytes / clen}
 
 
-def bench_lz4c(args, rank, world, n=None, fast=False, level=0):
-    """configs[2]: LZ4F compress (rd_kafka_lz4_compress semantics) of 1 MiB
-    JSON batches.  fast=False: frames byte-identical to the reference's;
-    fast=True: the throughput-mode encoder (reference-decodable frames, ratio
-    within 5 % of the reference's)."""
+def bench_lz4c(args, rank, world, n=None, fast=False, level=0, size=JSON_BATCH, units=False):
+    """configs[2]: LZ4F compress (rd_kafka_lz4_compress semantics) of JSON batches.
+    fast=False: frames byte-identical to the reference's; fast=True: the throughput-mode
+    encoder (reference-decodable frames, ratio within 5 % of the reference's); units=True:
+    the same contract on the workgroup-per-block engine (rdk_hip_lz4f_compress_units)."""
     import torch
     import librdkafka_amd as L
     n = n or args.partitions
-    src, offs, lens = json_batches(n, seed=42 + rank)
-    bound = (L.lz4f_compress_bound(JSON_BATCH) + 255) // 256 * 256
+    src, offs, lens = json_batches(n, size, seed=42 + rank)
+    bound = (L.lz4f_compress_bound(size) + 255) // 256 * 256
     dst = torch.empty(n * bound + 256, dtype=torch.uint8, device="cuda")
     ooffs = torch.arange(n, dtype=torch.int64, device="cuda") * bound
     olens = torch.zeros(n, dtype=torch.int32, device="cuda")
-    if fast:
+    if units:
+        comp = L.lz4f_compress_units_batch
+    elif fast:
         comp = L.lz4f_compress_fast_batch
     else:
         comp = lambda *a: L.lz4f_compress_batch(*a, level=level)  # noqa: E731
     ms, kms = _timed(lambda: comp(src, offs, lens, dst, ooffs, olens),
                      args.steps, args.warmup, world)
     clen = int(olens.sum())
-    return {"ms": ms, "kernel_ms": kms, "bytes": n * JSON_BATCH, "records": n,
-            "alg_bytes": n * JSON_BATCH + clen, "ratio": n * JSON_BATCH / clen,
+    return {"ms": ms, "kernel_ms": kms, "bytes": n * size, "records": n,
+            "alg_bytes": n * size + clen, "ratio": n * size / clen,
             "frames": (dst, ooffs, olens)}
 
 
@@ -378,39 +412,46 @@ def cpu_baseline_snappy(kind, n=64, seconds=4.0):
                       f"{'compress_fragment' if kind == 'compress' else 'decoder'} restated, {cpu_model()}"}
 
 
-def bench_consumer(args, rank, world, n=None):
+def bench_consumer(args, rank, world, n=None, size=JSON_BATCH):
     """configs[3]: consumer path per fetched v2 batch: CRC32C verify
     (check.crcs, rdkafka_msgset_reader.c:982-1015) then LZ4F decompress
-    (rdkafka_msgset_reader.c:393-407) of 1 MiB-record batches."""
+    (rdkafka_msgset_reader.c:393-407) of batches of `size` record bytes (frames made by the
+    exact compressor: byte-identical to the reference's)."""
     import numpy as np
     import torch
     import librdkafka_amd as L
     from librdkafka_amd import workload as W
     n = n or args.partitions
-    c = bench_lz4c(argparse.Namespace(steps=1, warmup=0, partitions=n), rank, world, n)
+    c = bench_lz4c(argparse.Namespace(steps=1, warmup=0, partitions=n), rank, world, n, size=size)
     frames, foffs, flens = c["frames"]
     fl = flens.cpu().numpy().astype(np.int64)
     slot = (61 + int(fl.max()) + 255) // 256 * 256
+    bound = int(foffs[1] - foffs[0]) if n > 1 else slot
     batches = torch.zeros(n * slot + 256, dtype=torch.uint8, device="cuda")
-    fo = foffs.cpu().numpy()
     hdrs = bytearray()
     for i in range(n):  # v2 header: Length, Attributes = LZ4 (3), RecordCount
         h = bytearray(W.v2_header(i, 64))
         h[8:12] = int(61 + fl[i] - 12).to_bytes(4, "big")
         h[21:23] = (3).to_bytes(2, "big")
         hdrs += h
-        batches[i * slot + 61:i * slot + 61 + fl[i]] = frames[fo[i]:fo[i] + fl[i]]
+    keep = min(bound, slot - 61)  # every frame is shorter than both
+    fv = frames[:n * bound].view(n, bound)[:, :keep]
+    bv = batches[:n * slot].view(n, slot)
+    for lo in range(0, n, 4096):
+        hi = min(n, lo + 4096)
+        bv[lo:hi, 61:61 + keep] = fv[lo:hi]
     hd = torch.frombuffer(hdrs, dtype=torch.uint8).cuda().view(n, 61)
-    batches[:n * slot].view(n, slot)[:, :61] = hd
+    bv[:, :61] = hd
     boffs = torch.arange(n, dtype=torch.int64, device="cuda") * slot
     bcaps = torch.full((n,), slot, dtype=torch.int32, device="cuda")
     crc_out = torch.zeros(n, dtype=torch.int32, device="cuda")
     L.msgset_v2_crc(batches, boffs, bcaps, crc_out, L.V2_CRC_FINALIZE)
     pay_offs = boffs + 61
     pay_lens = flens.clone()
-    out = torch.empty(n * JSON_BATCH + 256, dtype=torch.uint8, device="cuda")
-    ooffs = torch.arange(n, dtype=torch.int64, device="cuda") * JSON_BATCH
-    ocaps = torch.full((n,), JSON_BATCH, dtype=torch.int32, device="cuda")
+    dslot = (size + 255) // 256 * 256
+    out = torch.empty(n * dslot + 256, dtype=torch.uint8, device="cuda")
+    ooffs = torch.arange(n, dtype=torch.int64, device="cuda") * dslot
+    ocaps = torch.full((n,), dslot, dtype=torch.int32, device="cuda")
     olens = torch.zeros(n, dtype=torch.int32, device="cuda")
     st = torch.zeros(n, dtype=torch.int32, device="cuda")
 
@@ -419,12 +460,13 @@ def bench_consumer(args, rank, world, n=None):
         L.lz4f_decompress_batch(batches, pay_offs, pay_lens, out, ooffs, ocaps, olens, st)
 
     ms, kms = _timed(step, args.steps, args.warmup, world)
-    assert int(crc_out.abs().sum()) == 0 and int(st.abs().sum()) == 0
-    src, _, _ = json_batches(min(n, 8), seed=42 + rank)
-    assert torch.equal(out[:min(n, 8) * JSON_BATCH], src[:min(n, 8) * JSON_BATCH])
+    assert int(crc_out.abs().sum()) == 0 and int(st.abs().sum()) == 0 and bool((olens == size).all())
+    k = min(n, 8)
+    src, _, _ = json_batches(k, size, seed=42 + rank)
+    assert torch.equal(out[:k * dslot].view(k, dslot)[:, :size], src[:k * size].view(k, size))
     csum = int(fl.sum())
-    return {"ms": ms, "kernel_ms": kms, "bytes": n * JSON_BATCH, "records": n,
-            "alg_bytes": csum + (csum + 61 * n) + n * JSON_BATCH}
+    return {"ms": ms, "kernel_ms": kms, "bytes": n * size, "records": n,
+            "alg_bytes": csum + (csum + 61 * n) + n * size}
 
 
 def tiled_messages(n_batches, per_batch, seed=42):
@@ -620,6 +662,115 @@ def bench_chain(args, rank, world, n=None, per_batch=9500):
               # + header read and 40 B of row written per record by the index
               "alg_bytes": (clen + 61 * n) + clen + total + total + 61 * n + 40 * n * per_batch}
     return writer, reader
+
+
+def perf_tool_messages(msgs):
+    """configs[0]'s producer input: `rdkafka_performance -P -s 100 -c msgs -z lz4`
+    (examples/rdkafka_performance.c:798, :1318-1325), cut into MessageSets by write_msgq's
+    rule (rdkafka_msgset_writer.c:859-863, batch.num.messages 10000, message.max.bytes
+    1000000).  The messages are uniform, so the rule is run on the first MessageSet and the
+    others take its count."""
+    from librdkafka_amd import workload as W
+    m = W.gen_perf_messages(msgs)
+    head = {k: (v if k == "arena" else v[:12000]) for k, v in m.items()}
+    per = W.perf_batches(head)[0][1]
+    spec = [(f, min(per, msgs - f)) for f in range(0, msgs, per)]
+    return m, spec
+
+
+def bench_perf_tool(args, rank, world, msgs=1000000):
+    """configs[0]'s workload through the engine, device-resident: 1M x 100-byte messages of
+    the perf tool's payload -> record sizes + record writer (rdkafka_msgset_writer.c:652-754)
+    -> rdk_hip_msgset_v2_finalize with frames byte-identical to rd_kafka_lz4_compress ->
+    finished batches.  One step = all ~110 MessageSets (one broker thread's worth each).
+    Gate: CRC VERIFY, decompress, record index: every message comes back."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import librdkafka_amd as L
+    m, spec = perf_tool_messages(msgs)
+    n = len(spec)
+    d = {}
+    for k, v in m.items():
+        a = v.view(np.int64) if v.dtype == np.uint64 else (v.view(np.int32) if v.dtype == np.uint32 else v)
+        d[k] = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    b = np.zeros(n, dtype=L.V2_BATCH_DTYPE)
+    for i, (first, cnt) in enumerate(spec):
+        b[i] = (first, cnt, -1, -1, -1, 0)
+    sets, offs, sizes, _ = L.msgset_v2_build(d, b, crc=False)
+    mm = L._Msgs(*(d[k].data_ptr() for k in ("arena", "ts", "key_off", "key_len", "val_off",
+                                             "val_len", "hdr_off", "hdr_len", "hdr_cnt")))
+    rec_pos = torch.empty(msgs, dtype=torch.int32, device="cuda")
+    max_ts = torch.empty(n, dtype=torch.int64, device="cuda")
+    rec_offs, rec_lens = offs + 61, sizes - 61
+    rl = rec_lens.cpu().numpy().astype(np.int64)
+    cap = (61 + L.lz4f_compress_bound(int(rl.max())) + 255) // 256 * 256
+    out = torch.empty(n * cap + 256, dtype=torch.uint8, device="cuda")
+    out_offs = torch.arange(n, dtype=torch.int64, device="cuda") * cap
+    out_caps = torch.full((n,), cap, dtype=torch.int32, device="cuda")
+    flens, blens, crcs = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    s = L._stream(None)
+    lib = L.lib()
+
+    def step():
+        lib.rdk_hip_msgset_v2_sizes(C.byref(mm), b.ctypes.data, n, L._ptr(rec_pos), L._ptr(sizes),
+                                    L._ptr(max_ts), s)
+        lib.rdk_hip_msgset_v2_write(C.byref(mm), b.ctypes.data, n, L._ptr(rec_pos), L._ptr(sizes),
+                                    L._ptr(max_ts), L._ptr(offs), L._ptr(sets), None, s)
+        L.msgset_v2_finalize(sets, rec_offs, rec_lens, out, out_offs, out_caps, flens, blens, crcs,
+                             mode=L.PRODUCER_EXACT)
+
+    ms, kms = _timed(step, args.steps, args.warmup, world)
+    # gate: the reader side hands every message back
+    st, dl, ds, cnt = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(4))
+    L.msgset_v2_crc(out, out_offs, out_caps, st, L.V2_CRC_VERIFY)
+    dslot = (int(rl.max()) + 255) // 256 * 256
+    dec = torch.empty(n * dslot + 256, dtype=torch.uint8, device="cuda")
+    doffs = torch.arange(n, dtype=torch.int64, device="cuda") * dslot
+    dcaps = torch.full((n,), dslot, dtype=torch.int32, device="cuda")
+    L.lz4f_decompress_batch(out, out_offs + 61, flens, dec, doffs, dcaps, dl, ds)
+    row_offs = torch.tensor(np.asarray([f for f, _ in spec], np.int64), device="cuda")
+    row_caps = torch.tensor(np.asarray([c for _, c in spec], np.int32), device="cuda")
+    rows = {k: torch.empty(msgs, dtype=getattr(torch, t), device="cuda") for k, t in L.V2_ROW_FIELDS}
+    L.msgset_v2_index(out, out_offs, dec, doffs, dl, row_offs, row_caps, rows, cnt)
+    if int(st.abs().sum()) or int(ds.abs().sum()) or not bool((dl == rec_lens).all()) or \
+            cnt.cpu().tolist() != [c for _, c in spec] or not torch.equal(rows["timestamp"], d["ts"]) \
+            or not bool((rows["val_len"] == 100).all()):
+        raise SystemExit(f"rank {rank}: the perf-tool batches did not come back from the reader side")
+    if not bool((blens == flens + 61).all()):
+        raise SystemExit(f"rank {rank}: a perf-tool batch was left uncompressed")
+    total = int(rl.sum())
+    clen = int(flens.to(torch.int64).sum())
+    return {"ms": ms, "kernel_ms": kms, "bytes": total, "records": n, "messages": msgs,
+            "alg_bytes": 100 + 48 * msgs + 2 * (total + 61 * n) + clen + 2 * 61 * n,
+            "ratio": total / clen, "host_sample": (m, spec)}
+
+
+def cpu_baseline_perf_tool(m, spec, seconds=6.0):
+    """configs[0]'s producer-side work on ONE host core: the oracle's restatement of the v2
+    record writer (msgset_oracle.c), the reference's own compiled lz4frame.c / lz4.c driven as
+    rd_kafka_lz4_compress drives it (oracle/_ref; the restatement when it is not in the
+    tree), CRC32C of the finished batch (crc32c_hw restated)."""
+    import oracle
+    use_ref = oracle.ref_available()
+    done, nmsgs, t0 = 0, 0, time.perf_counter()
+    while True:
+        first, cnt = spec[done % len(spec)]
+        mset = oracle.msgset_v2_write(m, first, cnt, -1, -1, -1, 0)
+        err, frame = (oracle.ref_rdk_lz4_compress([mset[61:]]) if use_ref
+                      else oracle.rdk_lz4_compress(mset[61:]))
+        assert err == 0
+        oracle.crc32c_hw(0, mset[21:61] + frame)
+        done += 1
+        nmsgs += cnt
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(nmsgs / el, 1), "unit": "msgs/s", "cores": 1,
+            "kind": "reference" if use_ref else "port",
+            "sample": f"{done} MessageSets ({nmsgs} messages of 100 B) in {el:.1f} s: v2 record writer "
+                      f"restated + {'the reference lz4frame.c' if use_ref else 'lz4 restated'} + "
+                      f"CRC32C (crc32c_hw restated), {cpu_model()}"}
 
 
 def bench_legacy(args, rank, world, n=None, set_bytes=1 << 20):
@@ -1029,26 +1180,26 @@ def leg_line(name, res, steps, world, cpu=None):
 
 
 def index_leg(rank, world, no_cpu):
-    res = bench_index(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
+    res = bench_index(argparse.Namespace(steps=LEG_STEPS, warmup=2, partitions=256), rank, world)
     cpu = None if no_cpu else cpu_baseline_index(*res.pop("host_sample"))
     res.pop("host_sample", None)
-    return leg_line("v2_record_index_1MiB_json", res, 3, world, cpu)
+    return leg_line("v2_record_index_1MiB_json", res, LEG_STEPS, world, cpu)
 
 
 def legacy_leg(rank, world, no_cpu):
-    res = bench_legacy(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
+    res = bench_legacy(argparse.Namespace(steps=LEG_STEPS, warmup=2, partitions=256), rank, world)
     cpu = None if no_cpu else cpu_baseline_legacy(*res.pop("host_sample"))
     res.pop("host_sample", None)
-    d = leg_line("v1_msgset_crc32_verify_1MiB_json", res, 3, world, cpu)
+    d = leg_line("v1_msgset_crc32_verify_1MiB_json", res, LEG_STEPS, world, cpu)
     d["finalize_kernel_ms"] = res["finalize_kernel_ms"]
     return d
 
 
 def serialize_leg(rank, world, no_cpu):
-    res = bench_serialize(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world)
+    res = bench_serialize(argparse.Namespace(steps=LEG_STEPS, warmup=2, partitions=256), rank, world)
     cpu = None if no_cpu else cpu_baseline_serialize(*res.pop("host_sample"))
     res.pop("host_sample", None)
-    return leg_line("v2_record_serialize_1MiB_json", res, 3, world, cpu)
+    return leg_line("v2_record_serialize_1MiB_json", res, LEG_STEPS, world, cpu)
 
 
 # ------------------------------------------------------------------ main
@@ -1069,21 +1220,33 @@ def crc_leg(args, rank, world):
     return d, res
 
 
+SIZE_NAMES = {16384: "16KiB", 65536: "64KiB", 262144: "256KiB", 1 << 20: "1MiB"}
+LEG_STEPS = 10
+
+
+def finalize_leg_name(mode, size):
+    return f"writer_finalize{'_fast' if mode else ''}_{SIZE_NAMES[size]}_json"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="finalize",
-                    choices=["finalize", "finalize_fast", "crc", "lz4c", "lz4c_fast", "lz4hc",
-                             "consumer", "producer", "serialize", "index", "legacy", "snappyc",
-                             "snappyd"])
+    ap.add_argument("--workload", default="finalize_fast",
+                    choices=["finalize", "finalize_fast", "crc", "lz4c", "lz4c_fast", "lz4c_units",
+                             "lz4hc", "consumer", "producer", "serialize", "index", "legacy",
+                             "snappyc", "snappyd", "perf_tool", "chain_writer", "chain_reader"])
     ap.add_argument("--batches", type=int, default=CRC_BATCHES, help="--workload crc: batches per GPU")
     ap.add_argument("--partitions", type=int, default=512,
-                    help="toppars (1 MiB batches) per GPU")
+                    help="toppars (batches) per GPU")
+    ap.add_argument("--batch-bytes", type=int, default=JSON_BATCH, choices=sorted(SIZE_NAMES),
+                    help="record bytes per batch of the LZ4 workloads")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true")
     ap.add_argument("--level", type=int, default=9, help="compression.level of --workload lz4hc")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks than GPUs (ranks then share devices; labelled so)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1098,21 +1261,30 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    # one rank per GPU; with fewer GPUs than ranks (a rehearsal on one device) ranks share
-    device = local_rank % max(1, torch.cuda.device_count())
+    # one rank per GPU; with fewer GPUs than ranks (a rehearsal on one device) ranks share,
+    # and the line says so: n_gpus counts the devices actually used
+    ndev = max(1, torch.cuda.device_count())
+    device = local_rank % ndev
+    shared = world > ndev
+    if shared and not args.rehearsal:
+        sys.exit(f"bench.py: {world} ranks but {ndev} GPU(s): pass --rehearsal to let ranks share "
+                 f"devices (the line is then labelled shared_device, not a scaling point)")
+    gpus_used = min(world, ndev)
     torch.cuda.set_device(device)
     import librdkafka_amd as L
     if not os.path.exists(L.LIB_PATH):
         raise SystemExit(f"{L.LIB_PATH} is not built: run __graft_entry__.build()")
     L.init(device)
     no_cpu = args.no_cpu_baseline or world > 1
+    size = args.batch_bytes
+    where = {"n_gpus": gpus_used, "ranks": world, **({"shared_device": True} if shared else {})}
 
     def finish():
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
 
-    if args.workload not in ("finalize", "finalize_fast"):
+    if args.workload not in ("finalize", "finalize_fast") or size != JSON_BATCH:
         # single legs (profiling, A/B runs): one short JSON line
         if args.workload == "crc":
             d, res = crc_leg(args, rank, world)
@@ -1121,13 +1293,21 @@ def main():
                 d["GB_per_s"] = round(res["bytes"] * world / (t_max / 1e3) / 1e9, 2)
                 if not no_cpu:
                     d["cpu_baseline"] = cpu_baseline_crc(*res["host_sample"])
-                print(json.dumps({"workload": "crc", "n_gpus": world, "steps": args.steps,
+                print(json.dumps({"workload": "crc", **where, "steps": args.steps,
                                   "source_hash": source_hash(), **d}), flush=True)
             return finish()
-        if args.workload == "lz4hc":
+        name = LEG_NAMES.get(args.workload, args.workload)
+        if args.workload in ("finalize", "finalize_fast"):
+            mode = 1 if args.workload == "finalize_fast" else 0
+            res = bench_finalize(args, rank, world, n=args.partitions, mode=mode, size=size)
+            name = finalize_leg_name(mode, size)
+        elif args.workload == "lz4hc":
             res = bench_lz4c(args, rank, world, n=args.partitions, level=args.level)
+            name = f"lz4hc_compress_level{args.level}_1MiB_json"
         elif args.workload.startswith("lz4c"):
-            res = bench_lz4c(args, rank, world, n=args.partitions, fast=args.workload == "lz4c_fast")
+            res = bench_lz4c(args, rank, world, n=args.partitions, fast=args.workload == "lz4c_fast",
+                             units=args.workload == "lz4c_units", size=size)
+            name = name.replace("1MiB", SIZE_NAMES[size])
         elif args.workload == "producer":
             res = bench_producer(args, rank, world, n=args.partitions)
         elif args.workload == "serialize":
@@ -1136,11 +1316,17 @@ def main():
             res = bench_index(args, rank, world, n=args.partitions)
         elif args.workload == "legacy":
             res = bench_legacy(args, rank, world, n=args.partitions)
+        elif args.workload == "perf_tool":
+            res = bench_perf_tool(args, rank, world)
+        elif args.workload.startswith("chain"):
+            wr, rd = bench_chain(args, rank, world, n=args.partitions)
+            res = wr if args.workload == "chain_writer" else rd
         elif args.workload.startswith("snappy"):
             res = bench_snappy(args, rank, world, n=args.partitions,
                                decompress=args.workload == "snappyd")
         else:
-            res = bench_consumer(args, rank, world, n=args.partitions)
+            res = bench_consumer(args, rank, world, n=args.partitions, size=size)
+            name = name.replace("1MiB", SIZE_NAMES[size])
         t_max = max_over_ranks(res["ms"], world)
         if rank == 0:
             cpu = None
@@ -1151,40 +1337,56 @@ def main():
                     cpu = cpu_baseline_index(*res["host_sample"])
                 elif args.workload == "legacy":
                     cpu = cpu_baseline_legacy(*res["host_sample"])
+                elif args.workload == "perf_tool":
+                    cpu = cpu_baseline_perf_tool(*res["host_sample"])
                 elif args.workload.startswith("snappy"):
                     cpu = cpu_baseline_snappy("compress" if args.workload == "snappyc" else "decompress")
-                else:
+                elif not args.workload.startswith("chain"):
                     cpu = cpu_reference_lz4("decompress" if args.workload == "consumer"
                                             else "compress",
                                             level=args.level if args.workload == "lz4hc" else 0,
-                                            with_crc=args.workload == "consumer")
+                                            with_crc=args.workload in ("consumer", "finalize", "finalize_fast"))
             res.pop("host_sample", None)
             res["ms"] = t_max
-            print(json.dumps({"workload": args.workload, "n_gpus": world, "steps": args.steps,
+            print(json.dumps({"workload": args.workload, **where, "steps": args.steps,
                               "source_hash": source_hash(),
-                              **leg_line(f"lz4hc_compress_level{args.level}_1MiB_json"
-                                         if args.workload == "lz4hc" else
-                                         LEG_NAMES.get(args.workload, args.workload), res,
-                                         args.steps, world, cpu)}), flush=True)
+                              **leg_line(name, res, args.steps, world, cpu)}), flush=True)
         return finish()
 
     # ------------------------------------------------------------ headline
+    # north_star's bar for the compress half is "frames decode with the reference's
+    # rd_kafka_lz4_decompress, ratio within 5 % of the reference's": the throughput
+    # compressor (mode 1) meets it and is the headline; the byte-identical compressor is the
+    # leg writer_finalize_1MiB_json.
     mode = 1 if args.workload == "finalize_fast" else 0
     res = bench_finalize(args, rank, world, mode=mode)
     # whole-job time per step: max over ranks of the host clock around the K synchronised
-    # steps; the HIP-event time of the compress stage feeds the roofline
+    # steps; the HIP-event time of the step feeds the roofline
     t_max = max_over_ranks(res["ms"], world)
+    legs = {}
+    if world > 1 and not args.no_legs:
+        # configs[3] is quoted sharded over 2/4/8 GPUs: the consumer leg runs on every rank
+        cres = bench_consumer(argparse.Namespace(steps=LEG_STEPS, warmup=2, partitions=1024 // world),
+                              rank, world, n=1024 // world)
+        cres["ms"] = max_over_ranks(cres["ms"], world)
+        if rank == 0:
+            legs["consumer_crc_verify_lz4f_decompress_1MiB"] = leg_line(
+                "consumer_crc_verify_lz4f_decompress_1MiB_sharded", cres, LEG_STEPS, world)
     if rank == 0:
         n = res["records"]
         value = res["bytes"] * world / (t_max / 1e3) / 1e9
         achieved = res["alg_bytes"] / (res["kernel_ms"] / 1e3) / 1e9
-        leg = "writer_finalize_fast_1MiB_json" if mode else "writer_finalize_1MiB_json"
+        leg = finalize_leg_name(mode, JSON_BATCH)
         traffic, note = profile_summary(leg, res["alg_bytes"], res["kernel_ms"])
-        line = {
+        kernels = (("lz4_units_blocks_kernel + lz4f_assemble_kernel<finalize> + crc32c_msgset_v2 kernels"
+                    if os.environ.get("RDK_HIP_LZ4_FAST_ENGINE", "").startswith("u") else
+                    "lz4_fast_blocks_kernel + lz4f_assemble_kernel<finalize>") if mode else
+                   "lz4_compress_blocks_kernel<windows> + lz4f_assemble_kernel<finalize>")
+        head = {
             "metric": "record-batch GB/s (CRC32C+LZ4F) at 1/2/4/8 GPUs; % of HBM roofline",
             "value": round(value, 2),
             "unit": "GB/s",
-            "n_gpus": world,
+            **where,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t_max, 4),
@@ -1194,7 +1396,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded JSON-like records, valid v2 headers, device-resident)",
             "config": {"workload": "combined CRC32C+LZ4F, writer side: rdk_hip_msgset_v2_finalize = "
-                                   "LZ4F compress (" + ("throughput compressor, reference-decodable"
+                                   "LZ4F compress (" + ("throughput compressor: frames decode with the "
+                                                        "reference decoder, ratio within 5 % of the reference's"
                                                         if mode else
                                                         "frames byte-identical to rd_kafka_lz4_compress")
                                    + ") + v2 header finalize + CRC32C finalize of 1 MiB JSON "
@@ -1202,29 +1405,28 @@ def main():
                                    "value counts uncompressed record bytes",
                        "batches_per_gpu": n, "batch_bytes": JSON_BATCH,
                        "parallelism": f"toppar-sharded x{world}, no collective"},
-            "msgs_per_s": round(n * world * 9500 / (t_max / 1e3), 1),
+            "msgs_per_s": round(res["messages"] * world / (t_max / 1e3), 1),
+            "msgs_note": "JSON records (lines) carried by the batches, counted",
             "compression_ratio": round(res["ratio"], 3),
             "source_hash": source_hash(),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": ("lz4_fast_blocks_kernel" if mode else
-                                    "lz4_compress_blocks_kernel<windows>") +
-                                   " + lz4f_assemble_kernel<finalize> (the whole step)",
+                         "kernel": kernels + " (the whole step)",
                          "kernel_ms": round(res["kernel_ms"], 4),
                          "alg_bytes_per_launch": int(res["alg_bytes"]), **note},
             "cpu_baseline": None,
         }
         if not no_cpu:
-            line["cpu_baseline"] = cpu_reference_lz4("compress", seconds=10.0, with_crc=True)
+            head["cpu_baseline"] = cpu_reference_lz4("compress", seconds=10.0, with_crc=True)
         del res
         torch.cuda.empty_cache()
         if world == 1:
-            line["pcie_pinned"] = pcie_rates()
+            head["pcie_pinned"] = pcie_rates()
         if not args.no_legs and world == 1:
-            sub = argparse.Namespace(steps=3, warmup=1, partitions=256)
+            sub = argparse.Namespace(steps=LEG_STEPS, warmup=2, partitions=256)
             cpu = (lambda *a, **k: None) if no_cpu else cpu_reference_lz4
-            legs = {}
+            # configs[1]
             crc_args = argparse.Namespace(steps=10, warmup=2, batches=CRC_BATCHES)
             d, cres = crc_leg(crc_args, rank, world)
             if not no_cpu:
@@ -1232,63 +1434,108 @@ def main():
             del cres
             torch.cuda.empty_cache()
             legs["crc32c_only_16KiB_batches"] = d
-            other = bench_finalize(sub, rank, world, n=256, mode=1 - mode)
-            legs["writer_finalize_1MiB_json" if mode else "writer_finalize_fast_1MiB_json"] = leg_line(
-                "writer_finalize_1MiB_json" if mode else "writer_finalize_fast_1MiB_json",
-                other, 3, 1, cpu("compress", with_crc=True))
+            # configs[0]'s workload through the engine
+            pres = bench_perf_tool(sub, rank, world)
+            pcpu = None if no_cpu else cpu_baseline_perf_tool(*pres.pop("host_sample"))
+            pres.pop("host_sample", None)
+            pl = leg_line("perf_tool_1M_x_100B_messages", pres, LEG_STEPS, 1, pcpu)
+            pl["msgs_per_s"] = round(pres["messages"] / (pres["ms"] / 1e3), 1)
+            legs["perf_tool_1M_x_100B_messages"] = pl
+            del pres
+            torch.cuda.empty_cache()
+            # the other compressor on the headline's step
+            other = bench_finalize(sub, rank, world, n=512, mode=1 - mode)
+            legs[finalize_leg_name(1 - mode, JSON_BATCH)] = leg_line(
+                finalize_leg_name(1 - mode, JSON_BATCH), other, LEG_STEPS, 1,
+                cpu("compress", with_crc=True))
+            del other
+            # batch-size sweep of the combined step and of the consumer path, 512 MiB each
+            for bsz in (16384, 65536, 262144):
+                nb = (512 << 20) // bsz
+                for m_ in (1, 0):
+                    r_ = bench_finalize(sub, rank, world, n=nb, mode=m_, size=bsz)
+                    ll = leg_line(finalize_leg_name(m_, bsz), r_, LEG_STEPS, 1)
+                    ll["msgs_per_s"] = round(r_["messages"] / (r_["ms"] / 1e3), 1)
+                    legs[finalize_leg_name(m_, bsz)] = ll
+                    del r_
+                    torch.cuda.empty_cache()
+                r_ = bench_consumer(sub, rank, world, n=nb, size=bsz)
+                legs[f"consumer_crc_verify_lz4f_decompress_{SIZE_NAMES[bsz]}"] = leg_line(
+                    f"consumer_crc_verify_lz4f_decompress_{SIZE_NAMES[bsz]}", r_, LEG_STEPS, 1)
+                del r_
+                torch.cuda.empty_cache()
             legs["lz4f_compress_1MiB_json"] = leg_line(
-                "lz4f_compress_1MiB_json", bench_lz4c(sub, rank, world, n=256), 3, 1, cpu("compress"))
+                "lz4f_compress_1MiB_json", bench_lz4c(sub, rank, world, n=256), LEG_STEPS, 1, cpu("compress"))
             legs["lz4f_compress_fast_1MiB_json"] = leg_line(
-                "lz4f_compress_fast_1MiB_json", bench_lz4c(sub, rank, world, n=256, fast=True), 3, 1,
+                "lz4f_compress_fast_1MiB_json", bench_lz4c(sub, rank, world, n=256, fast=True), LEG_STEPS, 1,
                 cpu("compress"))
+            legs["lz4f_compress_units_1MiB_json"] = leg_line(
+                "lz4f_compress_units_1MiB_json", bench_lz4c(sub, rank, world, n=256, units=True), LEG_STEPS, 1)
             # LZ4HC at its default level (LZ4HC_CLEVEL_DEFAULT = 9)
             legs["lz4hc_compress_level9_1MiB_json"] = leg_line(
-                "lz4hc_compress_level9_1MiB_json", bench_lz4c(sub, rank, world, n=256, level=9), 3, 1,
+                "lz4hc_compress_level9_1MiB_json", bench_lz4c(sub, rank, world, n=256, level=9), LEG_STEPS, 1,
                 cpu("compress", level=9))
             # LZ4HC optimal parser at its top level (LZ4HC_CLEVEL_MAX = 12)
             legs["lz4hc_compress_level12_1MiB_json"] = leg_line(
                 "lz4hc_compress_level12_1MiB_json",
-                bench_lz4c(argparse.Namespace(steps=2, warmup=1, partitions=256), rank, world, n=256,
-                           level=12), 2, 1, cpu("compress", level=12))
+                bench_lz4c(argparse.Namespace(steps=3, warmup=1, partitions=256), rank, world, n=256,
+                           level=12), 3, 1, cpu("compress", level=12))
             legs["snappy_compress_1MiB_json"] = leg_line(
-                "snappy_compress_1MiB_json", bench_snappy(sub, rank, world, n=256), 3, 1,
+                "snappy_compress_1MiB_json", bench_snappy(sub, rank, world, n=256), LEG_STEPS, 1,
                 None if no_cpu else cpu_baseline_snappy("compress"))
             legs["snappy_uncompress_1MiB_json"] = leg_line(
                 "snappy_uncompress_1MiB_json",
-                bench_snappy(argparse.Namespace(steps=3, warmup=1, partitions=1024), rank, world,
-                             n=1024, decompress=True), 3, 1,
+                bench_snappy(argparse.Namespace(steps=LEG_STEPS, warmup=2, partitions=1024), rank, world,
+                             n=1024, decompress=True), LEG_STEPS, 1,
                 None if no_cpu else cpu_baseline_snappy("decompress"))
             legs["consumer_crc_verify_lz4f_decompress_1MiB"] = leg_line(
                 "consumer_crc_verify_lz4f_decompress_1MiB",
-                bench_consumer(argparse.Namespace(steps=3, warmup=1, partitions=1024), rank, world,
-                               n=1024), 3, 1, cpu("decompress", with_crc=True))
+                bench_consumer(argparse.Namespace(steps=LEG_STEPS, warmup=2, partitions=1024), rank, world,
+                               n=1024), LEG_STEPS, 1, cpu("decompress", with_crc=True))
             legs["v2_record_serialize_1MiB_json"] = serialize_leg(rank, world, no_cpu)
             legs["v2_record_index_1MiB_json"] = index_leg(rank, world, no_cpu)
             legs["v1_msgset_crc32_verify_1MiB_json"] = legacy_leg(rank, world, no_cpu)
             wr, rd = bench_chain(sub, rank, world, n=256)
             legs["writer_messages_to_batches_1MiB_json"] = leg_line(
-                "writer_messages_to_batches_1MiB_json", wr, 3, 1)
+                "writer_messages_to_batches_1MiB_json", wr, LEG_STEPS, 1)
             legs["reader_batches_to_rows_1MiB_json"] = leg_line(
-                "reader_batches_to_rows_1MiB_json", rd, 3, 1)
-            legs["producer_pipeline_1MiB_json_pcie"] = leg_line(
-                "producer_pipeline_1MiB_json_pcie",
-                bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512), rank, world,
-                               n=512), 2, 1, cpu("compress", with_crc=True))
+                "reader_batches_to_rows_1MiB_json", rd, LEG_STEPS, 1)
+            prod = {}
+            for th in (1, 2, 4, 8):
+                pr = bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512), rank, world,
+                                    n=512, threads=th, slot_mib=max(32, 128 // th))
+                prod[f"{th}_threads"] = round(pr["bytes"] / (pr["ms"] / 1e3) / 1e9, 2)
+                if th == 1 or prod[f"{th}_threads"] >= max(prod.values()):
+                    best = pr
+            pl = leg_line("producer_pipeline_1MiB_json_pcie", best, 2, 1, cpu("compress", with_crc=True))
+            pl["GB_per_s_by_host_threads"] = prod
+            legs["producer_pipeline_1MiB_json_pcie"] = pl
             if not no_cpu:
                 legs["dropin_per_call_us"] = bench_dropin_calls()
-            line["legs"] = legs
+        # the legs first: whoever keeps only the end of this line keeps the headline
+        line = {"legs": legs, **head} if legs else head
+        # configs[1] once more among the last keys, where a truncated tail still shows it
+        if "crc32c_only_16KiB_batches" in legs:
+            c = legs["crc32c_only_16KiB_batches"]
+            line["crc32c_only_16KiB_batches"] = {"GB_per_s": c["GB_per_s"], "frac": c["roofline"]["frac"],
+                                                 "kernel_ms": c["roofline"]["kernel_ms"],
+                                                 "traffic": c["roofline"]["traffic"]}
         print(json.dumps(line), flush=True)
     finish()
 
 
-# bench leg name of a single --workload run (profiles/r02/<leg>.json)
+# bench leg name of a single --workload run (profiles/r03/<leg>.json)
 LEG_NAMES = {"lz4c": "lz4f_compress_1MiB_json", "lz4c_fast": "lz4f_compress_fast_1MiB_json",
+             "lz4c_units": "lz4f_compress_units_1MiB_json",
              "lz4hc": "lz4hc_compress_level9_1MiB_json",
              "consumer": "consumer_crc_verify_lz4f_decompress_1MiB",
              "serialize": "v2_record_serialize_1MiB_json", "index": "v2_record_index_1MiB_json",
              "legacy": "v1_msgset_crc32_verify_1MiB_json",
              "snappyc": "snappy_compress_1MiB_json", "snappyd": "snappy_uncompress_1MiB_json",
-             "producer": "producer_pipeline_1MiB_json_pcie"}
+             "producer": "producer_pipeline_1MiB_json_pcie",
+             "perf_tool": "perf_tool_1M_x_100B_messages",
+             "chain_writer": "writer_messages_to_batches_1MiB_json",
+             "chain_reader": "reader_batches_to_rows_1MiB_json"}
 
 
 if __name__ == "__main__":

@@ -1,8 +1,9 @@
-"""Summarise one leg's rocprofv3 passes (scripts/profile_r2.sh) into profiles/r02/<leg>.json.
+"""Summarise one leg's rocprofv3 passes (scripts/profile_r3.sh) into profiles/r03/<leg>.json.
 
   DIR/trace/**/*kernel_trace.csv          rocprofv3 --kernel-trace --stats
   DIR/pmc_fetch/**/*counter_collection.csv  rocprofv3 --pmc FETCH_SIZE
   DIR/pmc_write/**/*counter_collection.csv  rocprofv3 --pmc WRITE_SIZE
+  DIR/pmc_sq/**/*counter_collection.csv     rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU ... (optional)
   DIR/bench.json                          the bench line of the traced run
 
 A leg's step may be several kernels (KERNELS = comma-separated name substrings), some of them
@@ -43,6 +44,8 @@ def main(d, leg, kernels, out):
     trace = rows(os.path.join(d, "trace", "**", "*kernel_trace.csv"))
     fetch = rows(os.path.join(d, "pmc_fetch", "**", "*counter_collection.csv"))
     write = rows(os.path.join(d, "pmc_write", "**", "*counter_collection.csv"))
+    sq = rows(os.path.join(d, "pmc_sq", "**", "*counter_collection.csv"))
+    sq_tot = {}
     tot_ns = tot_fetch = tot_write = 0.0
     have_pmc = True
     # a step may launch a kernel several times (the LZ4HC engine runs in chunks): the kernel
@@ -68,6 +71,11 @@ def main(d, leg, kernels, out):
             tot_write += e["write_bytes"]
         else:
             have_pmc = False
+        for cname in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY"):
+            v = [float(r["Counter_Value"]) for r in sq if k in r["Kernel_Name"] and r["Counter_Name"] == cname]
+            if v:
+                e[cname.lower()] = sum(v) / steps
+                sq_tot[cname] = sq_tot.get(cname, 0.0) + e[cname.lower()]
         tot_ns += e["avg_ns"]
         s["kernels"][k] = e
     s["avg_ns"] = tot_ns
@@ -75,7 +83,18 @@ def main(d, leg, kernels, out):
         s["fetch_bytes"], s["write_bytes"] = tot_fetch, tot_write
         s["traffic_bytes"] = tot_fetch + tot_write
         s["traffic_over_alg"] = s["traffic_bytes"] / s["alg_bytes_per_launch"]
+    if "SQ_INSTS_VALU" in sq_tot:
+        # the issue ceiling: one wave64 vector instruction per SIMD per 4 cycles
+        s["valu_insts"] = sq_tot["SQ_INSTS_VALU"]
+        s["salu_insts"] = sq_tot.get("SQ_INSTS_SALU")
+        s["lds_insts"] = sq_tot.get("SQ_INSTS_LDS")
+        s["valu_insts_per_64_alg_bytes"] = s["valu_insts"] * 64.0 / s["alg_bytes_per_launch"]
+        s["issue_floor_ns"] = s["valu_insts"] * 4.0 / (1024 * 2.4)
+        if sq_tot.get("SQ_WAVE_CYCLES"):
+            s["wait_any_over_wave_cycles"] = sq_tot.get("SQ_WAIT_ANY", 0.0) / sq_tot["SQ_WAVE_CYCLES"]
     if tot_ns:
+        if "issue_floor_ns" in s:
+            s["frac_of_issue_ceiling"] = s["issue_floor_ns"] / tot_ns
         s["achieved_GBps_alg"] = s["alg_bytes_per_launch"] / tot_ns
         s["frac_of_8TBps"] = s["achieved_GBps_alg"] / 8000.0
     os.makedirs(os.path.dirname(out), exist_ok=True)

@@ -104,14 +104,23 @@ def test_two_ranks_run_the_engine_on_their_shards(oracle_mod):
 
 @pytest.mark.timeout(900)
 def test_bench_gpus_2_launches_two_ranks():
-    """bench.py --gpus 2 started by hand: the parent launches two ranks (both on device 0
-    when the box has one GPU) and rank 0 reports n_gpus 2 (weak scaling: 16 batches per rank); a --gpus that contradicts WORLD_SIZE is refused."""
+    """bench.py --gpus 2 started by hand: the parent launches two ranks and rank 0 reports
+    ranks 2 (weak scaling: 16 batches per rank).  On a box with one GPU the ranks share it:
+    that takes --rehearsal, and the line then counts one GPU and says shared_device, so it
+    cannot pass for a scaling point.  A --gpus that contradicts WORLD_SIZE is refused."""
+    import torch
+    ndev = torch.cuda.device_count()
     common = ["--steps", "3", "--warmup", "1", "--partitions", "16", "--no-legs", "--no-cpu-baseline"]
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + common,
+    if ndev < 2:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + common,
+                           capture_output=True, text=True, timeout=800, cwd=ROOT)
+        assert r.returncode != 0 and "--rehearsal" in r.stderr     # refused without the flag
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearsal"] + common,
                        capture_output=True, text=True, timeout=800, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["value"] > 0
+    assert line["ranks"] == 2 and line["n_gpus"] == min(2, ndev) and line["value"] > 0
+    assert line.get("shared_device", False) == (ndev < 2) and line["scaling"] == "weak"
     assert line["config"]["batches_per_gpu"] == 16
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + common,

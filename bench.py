@@ -1093,15 +1093,29 @@ def cpu_reference_lz4(kind, n=64, seconds=4.0, level=0, with_crc=False):
             "sample": f"{n} x 1 MiB JSON batches, {passes} passes, {what}, {cpu_model()}"}
 
 
-def bench_dropin_calls(seconds=0.4):
+def dropin_threads_lib():
+    """bench_native/libdropin_threads.so: pthreads calling one drop-in symbol through a function
+    pointer (built by __graft_entry__.build())."""
+    import ctypes as C
+    h = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench_native",
+                            "libdropin_threads.so"))
+    h.dropin_threads_run.restype = C.c_double
+    h.dropin_threads_run.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32,
+                                     C.c_size_t, C.c_int, C.c_double]
+    return h
+
+
+def bench_dropin_calls(seconds=0.3, cpu=True, thread_counts=(1, 8)):
     """Per-call cost of the drop-in symbols (host buffer in, host result out: gather into
     pinned staging, H2D, kernels, D2H, stream synchronise) at the reference's batch sizes,
-    beside the reference's compiled code on one host core.  Microseconds per call."""
+    called from 1 and from 8 native threads at once (wall time / calls of all threads: the
+    broker threads' concurrent calls go to the device together), beside the reference's
+    compiled code on one host core.  Microseconds per call."""
     import ctypes as C
-    import numpy as np
     import oracle
     import librdkafka_amd as L
     lib, olib, R = L.lib(), oracle.lib(), oracle.ref()
+    T = dropin_threads_lib()
     out = {}
 
     def per_call(fn):
@@ -1114,25 +1128,31 @@ def bench_dropin_calls(seconds=0.4):
             if el >= seconds:
                 return round(el / calls * 1e6, 1)
 
+    def fptr(f):
+        return C.cast(f, C.c_void_p)
+
+    before = L.dropin_combined()
     for size in (16384, 65536, 1 << 20):
         data = L.gen_json(size, 7)
         buf = C.create_string_buffer(data, size)
-        row = {}
-        row["crc32c_gpu_us"] = per_call(lambda: lib.crc32c(0, buf, size))
-        row["crc32c_cpu_us"] = per_call(lambda: olib.or_crc32c_hw(0, buf, size))
-        segs = [data[:61], data[61:]]
-        sl = L.RdSlice(segs)
-
-        def slice_crc():
-            sl.slice.seg = C.pointer(sl._segs[0])
-            sl.slice.rof = 0
-            return lib.rd_slice_crc32c(sl.ptr)
-        row["rd_slice_crc32c_gpu_us"] = per_call(slice_crc)
         err, frame = L.rd_kafka_lz4_compress(1, 0, data)
         assert err == 0
-        row["lz4_compress_gpu_us"] = per_call(lambda: L.rd_kafka_lz4_compress(1, 0, data))
-        row["lz4_decompress_gpu_us"] = per_call(lambda: L.rd_kafka_lz4_decompress(1, 0, frame))
-        if R is not None:
+        fbuf = C.create_string_buffer(frame, len(frame))
+        crc = oracle.crc32c(0, data)
+        row = {}
+        for th in thread_counts:
+            tag = "gpu_us" if th == 1 else f"gpu_us_{th}_threads"
+            for name, which, fn, b, n, xl in (
+                    ("crc32c", 0, lib.crc32c, buf, size, 0),
+                    ("rd_slice_crc32c", 1, lib.rd_slice_crc32c, buf, size, 0),
+                    ("lz4_compress", 2, lib.rd_kafka_lz4_compress, buf, size, len(frame)),
+                    ("lz4_decompress", 3, lib.rd_kafka_lz4_decompress, fbuf, len(frame), size)):
+                us = T.dropin_threads_run(which, fptr(fn), b, n, crc, xl, th, seconds)
+                assert us > 0, f"{name} x {th} threads at {size} B: wrong result"
+                row[f"{name}_{tag}"] = round(us, 1)
+        if cpu:
+            row["crc32c_cpu_us"] = per_call(lambda: olib.or_crc32c_hw(0, buf, size))
+        if cpu and R is not None:
             seg = C.c_char_p(data)
             sl1 = C.c_size_t(size)
             o, ol, g = C.c_void_p(), C.c_size_t(), C.c_int()
@@ -1141,7 +1161,6 @@ def bench_dropin_calls(seconds=0.4):
                 assert R.ref_rdk_lz4_compress(1, 0, C.byref(seg), C.byref(sl1), 1, C.byref(o),
                                               C.byref(ol)) == 0
                 R.ref_free(o)
-            fbuf = C.create_string_buffer(frame, len(frame))
 
             def ref_d():
                 assert R.ref_rdk_lz4_decompress(1, fbuf, len(frame), 1 << 30, C.byref(o),
@@ -1150,12 +1169,31 @@ def bench_dropin_calls(seconds=0.4):
             row["lz4_compress_cpu_us"] = per_call(ref_c)
             row["lz4_decompress_cpu_us"] = per_call(ref_d)
         out[f"{size}B"] = row
-    del np
+    after = L.dropin_combined()
+    nb, nr = after[0] - before[0], after[1] - before[1]
+    out["combined"] = {"batches": nb, "requests_per_batch": round(nr / nb, 2) if nb else 0,
+                       "largest": after[2], "fallbacks": after[3] - before[3],
+                       "enabled": os.environ.get("RDK_HIP_COMBINE", "1") != "0"}
     out["note"] = ("gpu: drop-in symbol through the C ABI on a host buffer (PCIe round trip + "
-                   "synchronise per call, includes the Python/ctypes call overhead of ~1-3 us); "
+                   "synchronise per launch), called by native threads in a loop, wall time / all "
+                   "threads' calls; concurrent calls are served as one launch (combined); "
                    "cpu: the reference's compiled lz4frame.c (kind reference) and crc32c_hw "
                    "restated (port), one core, " + cpu_model())
     return out
+
+
+def dropin_uncombined_columns():
+    """The 8-thread columns once more with RDK_HIP_COMBINE=0 (every call on its own thread's
+    stream), in a child process: the switch is read once per process."""
+    import subprocess
+    p = subprocess.run([sys.executable, os.path.abspath(__file__), "--workload", "dropin", "--no-cpu-baseline"],
+                       env=dict(os.environ, RDK_HIP_COMBINE="0"), capture_output=True, text=True,
+                       timeout=300)
+    if p.returncode:
+        return {"error": p.stderr[-300:]}
+    rows = json.loads(p.stdout.strip().splitlines()[-1])
+    return {k: {n: v for n, v in row.items() if n.endswith("_threads")}
+            for k, row in rows.items() if k.endswith("B")}
 
 
 def leg_line(name, res, steps, world, cpu=None):
@@ -1236,7 +1274,8 @@ def main():
     ap.add_argument("--workload", default="finalize_fast",
                     choices=["finalize", "finalize_fast", "crc", "lz4c", "lz4c_fast", "lz4c_units",
                              "lz4hc", "consumer", "producer", "serialize", "index", "legacy",
-                             "snappyc", "snappyd", "perf_tool", "chain_writer", "chain_reader"])
+                             "snappyc", "snappyd", "perf_tool", "chain_writer", "chain_reader",
+                             "dropin"])
     ap.add_argument("--batches", type=int, default=CRC_BATCHES, help="--workload crc: batches per GPU")
     ap.add_argument("--partitions", type=int, default=512,
                     help="toppars (batches) per GPU")
@@ -1286,6 +1325,9 @@ def main():
 
     if args.workload not in ("finalize", "finalize_fast") or size != JSON_BATCH:
         # single legs (profiling, A/B runs): one short JSON line
+        if args.workload == "dropin":
+            print(json.dumps(bench_dropin_calls(cpu=not no_cpu)), flush=True)
+            return finish()
         if args.workload == "crc":
             d, res = crc_leg(args, rank, world)
             t_max = max_over_ranks(d["ms_per_step"], world)
@@ -1512,6 +1554,7 @@ def main():
             legs["producer_pipeline_1MiB_json_pcie"] = pl
             if not no_cpu:
                 legs["dropin_per_call_us"] = bench_dropin_calls()
+                legs["dropin_per_call_us"]["uncombined_8_threads"] = dropin_uncombined_columns()
         # the legs first: whoever keeps only the end of this line keeps the headline
         line = {"legs": legs, **head} if legs else head
         # configs[1] once more among the last keys, where a truncated tail still shows it

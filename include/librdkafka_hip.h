@@ -107,6 +107,19 @@ void rdk_hip_dropin_calls(uint64_t out[5]);
 /* How many CRC drop-in calls finished on the host after the device path failed twice
  * (see the error contract at the top).  0 in a healthy process; the GPU tests assert it. */
 uint64_t rdk_hip_dropin_host_crcs(void);
+/* Concurrent calls of the symbols above from several threads (librdkafka's broker threads,
+ * rdkafka_broker.c:5082) are served together: a thread that finds no batch in flight takes
+ * every request queued so far to the device as one staging copy and one launch of each
+ * batch kernel; a thread that is about to serve fewer requests than the previous batch held
+ * waits at most RDK_HIP_COMBINE_WAIT_US microseconds (default 50; linger.ms is 500,
+ * rdkafka_conf.c:1095) for the others; a lone caller never waits.  CRC and decompress
+ * requests above 128 KiB go on their own thread's stream (their host copies dominate and
+ * run in parallel that way).  RDK_HIP_COMBINE=0 turns
+ * this off (every call on its own thread's stream).  out[0] = batches of two or more
+ * requests so far, out[1] = requests served in them, out[2] = the largest batch, out[3] =
+ * batches that fell back to one request at a time after a device error.  No counterpart
+ * in the reference. */
+void rdk_hip_dropin_combined(uint64_t out[4]);
 /* Engine contexts created / destroyed so far.  Every calling thread gets one context (HIP
  * stream, pinned staging, device scratch) on its first call; it is released when the
  * thread exits, as librdkafka's broker threads do (rdkafka_broker.c:5082).  No

@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "rd_kafka_snappy_uncompressed_length", "rd_kafka_snappy_compress_iov",
     "rd_kafka_snappy_compress", "rd_kafka_snappy_uncompress", "rd_kafka_snappy_java_uncompress",
     "rdk_hip_snappy_dropin_calls", "rdk_hip_dropin_host_crcs", "rdk_hip_ctx_counts",
+    "rdk_hip_dropin_combined",
     "rdk_hip_lz4f_compress_units",
 )
 
@@ -146,6 +147,8 @@ def lib():
     L.rdk_hip_dropin_host_crcs.argtypes = []
     L.rdk_hip_ctx_counts.restype = None
     L.rdk_hip_ctx_counts.argtypes = [vp]
+    L.rdk_hip_dropin_combined.restype = None
+    L.rdk_hip_dropin_combined.argtypes = [vp]
     _lib = L
     return L
 
@@ -302,6 +305,14 @@ def rd_kafka_lz4_decompress(proper_hc: int, offset: int, frame) -> tuple[int, by
 def dropin_host_crcs() -> int:
     """CRC drop-in calls that finished on the host after the device path failed twice."""
     return int(lib().rdk_hip_dropin_host_crcs())
+
+
+def dropin_combined() -> tuple[int, int, int, int]:
+    """(batches of >= 2 drop-in requests, requests served in them, largest batch, batches that
+    fell back to single requests after a device error)."""
+    a = (C.c_uint64 * 4)()
+    lib().rdk_hip_dropin_combined(a)
+    return tuple(int(x) for x in a)
 
 
 def ctx_counts() -> tuple[int, int]:

@@ -120,7 +120,8 @@ void crc_build_tables_v4(uint32_t *out, uint32_t poly) {
 
 // x2n[k] = x^(2^k) mod P in reflected form (bit 31 = x^0), for the
 // multiply-mod-P shift used when combining ranges of arbitrary length.
-static uint32_t multmodp(uint32_t a, uint32_t b, uint32_t poly) {
+uint32_t crc_multmodp(uint32_t a, uint32_t b, uint32_t poly) {
+  if (!a) return 0;  // the loop below ends at a's lowest set bit
   uint32_t m = 1u << 31, p = 0;
   for (;;) {
     if (a & m) {
@@ -136,7 +137,15 @@ static uint32_t multmodp(uint32_t a, uint32_t b, uint32_t poly) {
 void crc_build_x2n(uint32_t *out, uint32_t poly) {
   uint32_t p = 1u << 30;  // x^1
   out[0] = p;
-  for (int k = 1; k < 64; ++k) out[k] = p = multmodp(p, p, poly);
+  for (int k = 1; k < 64; ++k) out[k] = p = crc_multmodp(p, p, poly);
+}
+
+// x^(8 * nbytes) mod P from the x2n table (bit k of the bit count selects x2n[k])
+uint32_t crc_x_pow_bytes(const uint32_t x2n[64], uint64_t nbytes, uint32_t poly) {
+  uint32_t p = 1u << 31;  // x^0
+  for (int k = 3; nbytes; nbytes >>= 1, ++k)
+    if (nbytes & 1u) p = crc_multmodp(x2n[k], p, poly);
+  return p;
 }
 
 }  // namespace rdk

@@ -96,5 +96,10 @@ void crc_build_tables_v4(uint32_t *out /* kCrcV4Words */, uint32_t poly = kCrcPo
 // Host GF(2) helpers (also used by unit tests through the engine API).
 uint32_t crc_gf2_times(const uint32_t mat[32], uint32_t vec);
 void crc_zeros_operator(uint32_t op[32], size_t nbytes, uint32_t poly = kCrcPoly);
+// a * b mod P, reflected form (bit 31 = x^0); x^(8 * nbytes) mod P from a crc_build_x2n
+// table.  With them crc(init, A || B) == crc(0, B) ^ crc(init, A) * x^(8|B|): partial CRCs
+// of the pieces of a buffer combine on the host.
+uint32_t crc_multmodp(uint32_t a, uint32_t b, uint32_t poly = kCrcPoly);
+uint32_t crc_x_pow_bytes(const uint32_t x2n[64], uint64_t nbytes, uint32_t poly = kCrcPoly);
 
 }  // namespace rdk

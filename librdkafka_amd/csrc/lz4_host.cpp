@@ -74,6 +74,49 @@ size_t hc_offset(const uint8_t *b, size_t len) {
 }
 }  // namespace
 
+// rd_kafka_lz4_decompress_fixup_bad_framing (rdkafka_lz4.c:50-98): recompute HC in place
+int lz4f_fix_hc_in(uint8_t *in, size_t inlen) {
+  const size_t of = hc_offset(in, inlen);
+  if (!of) return kErrBadCompression;
+  in[of] = uint8_t((xxh32_small(in + 4, of - 4) >> 8) & 0xFFu);
+  return 0;
+}
+
+// rd_kafka_lz4_compress_break_framing (rdkafka_lz4.c:108-155): the legacy (wrong) HC
+int lz4f_break_hc_out(uint8_t *o, size_t flen) {
+  const size_t of = hc_offset(o, flen);
+  if (!of) return kErrBadCompression;
+  o[of] = uint8_t((xxh32_small(o, of) >> 8) & 0xFFu);
+  return 0;
+}
+
+// Output capacity for one frame in host memory, from a walk of its block headers.
+// Two sizings: `tight` = what the blocks can yield at most (lz4f_block_most), `slots` =
+// the in-place layout of independent blocks (block k at k * max_block).  The slot layout
+// is used when it costs at most 4x the tight bound (+ 1 MiB): every frame the reference's
+// writer makes.  A small frame of many short blocks of a large block class would
+// otherwise ask for gigabytes of staging; it gets the tight size and the device decodes
+// it in stream order.  Returns 0 or the frame's error.
+int lz4f_frame_capacity(const uint8_t *in, size_t inlen, uint64_t *cap_out) {
+  if (inlen > 0xFFFFFFFFull) return kErrBadCompression;
+  FrameWalker<HostReader> wk{HostReader{in}, inlen};
+  wk.header();
+  BlockInfo b;
+  uint64_t tight = 0, slots = 0, last_most = 0;
+  uint32_t nb = 0;
+  while (wk.next(b)) {
+    last_most = lz4f_block_most(b, wk.fi.max_block);
+    tight += last_most;
+    ++nb;
+  }
+  if (nb) slots = uint64_t(nb - 1) * wk.fi.max_block + last_most;
+  const uint64_t cap = (slots <= 4 * tight + (1u << 20)) ? (slots > tight ? slots : tight) : tight;
+  if (wk.fi.status) return wk.fi.status;
+  if (cap > 0xFFFFFFF0ull) return RDK_HIP_RESP_ERR__CRIT_SYS_RESOURCE;
+  *cap_out = cap;
+  return 0;
+}
+
 int lz4f_compress_host(Ctx *c, size_t len, int proper_hc, int level, void **out, size_t *outlen) {
   if (len > 0xFFFFFFFFull) return kErrBadCompression;
   const size_t bound = lz4f_compress_bound(len);
@@ -108,13 +151,9 @@ int lz4f_compress_host(Ctx *c, size_t len, int proper_hc, int level, void **out,
   uint8_t *o = static_cast<uint8_t *>(std::malloc(flen));
   if (!o) return RDK_HIP_RESP_ERR__CRIT_SYS_RESOURCE;
   std::memcpy(o, c->h_stage, flen);
-  if (!proper_hc) {  // rd_kafka_lz4_compress_break_framing (rdkafka_lz4.c:108-155)
-    const size_t of = hc_offset(o, flen);
-    if (!of) {
-      std::free(o);
-      return kErrBadCompression;
-    }
-    o[of] = uint8_t((xxh32_small(o, of) >> 8) & 0xFFu);
+  if (!proper_hc && (rc = lz4f_break_hc_out(o, flen))) {
+    std::free(o);
+    return rc;
   }
   *out = o;
   *outlen = flen;
@@ -123,36 +162,11 @@ int lz4f_compress_host(Ctx *c, size_t len, int proper_hc, int level, void **out,
 
 int lz4f_decompress_host(Ctx *c, int proper_hc, uint8_t *in, size_t inlen, void **out,
                          size_t *outlen) {
-  if (!proper_hc) {  // rd_kafka_lz4_decompress_fixup_bad_framing (rdkafka_lz4.c:50-98)
-    const size_t of = hc_offset(in, inlen);
-    if (!of) return kErrBadCompression;
-    in[of] = uint8_t((xxh32_small(in + 4, of - 4) >> 8) & 0xFFu);
-  }
-  if (inlen > 0xFFFFFFFFull) return kErrBadCompression;
-  // size the output from the block table (host walk of the frame headers)
-  FrameWalker<HostReader> wk{HostReader{in}, inlen};
-  wk.header();
-  BlockInfo b;
-  uint64_t cap = 0;
-  // Two sizings: `tight` = what the blocks can yield at most (lz4f_block_most), `slots` =
-  // the in-place layout of independent blocks (block k at k * max_block).  The slot layout
-  // is used when it costs at most 4x the tight bound (+ 1 MiB): every frame the reference's
-  // writer makes.  A small frame of many short blocks of a large block class would
-  // otherwise ask for gigabytes of staging; it gets the tight size and the device decodes
-  // it in stream order.
-  uint64_t tight = 0, slots = 0, last_most = 0;
-  uint32_t nb = 0;
-  while (wk.next(b)) {
-    last_most = lz4f_block_most(b, wk.fi.max_block);
-    tight += last_most;
-    ++nb;
-  }
-  if (nb) slots = uint64_t(nb - 1) * wk.fi.max_block + last_most;
-  cap = (slots <= 4 * tight + (1u << 20)) ? (slots > tight ? slots : tight) : tight;
-  if (wk.fi.status) return wk.fi.status;
-  if (cap > 0xFFFFFFF0ull) return RDK_HIP_RESP_ERR__CRIT_SYS_RESOURCE;
-  const size_t in_bytes = (inlen + 255) & ~size_t(255);
   int rc;
+  if (!proper_hc && (rc = lz4f_fix_hc_in(in, inlen))) return rc;
+  uint64_t cap = 0;
+  if ((rc = lz4f_frame_capacity(in, inlen, &cap))) return rc;
+  const size_t in_bytes = (inlen + 255) & ~size_t(255);
   if ((rc = ensure_host(c, inlen > cap ? inlen : cap)) ||
       (rc = ensure_dev(c, 0, in_bytes + cap + 64)) || (rc = ensure_desc(c, 128)))
     return rc;

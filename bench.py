@@ -897,7 +897,8 @@ def bench_producer(args, rank, world, n=None, threads=None, mode=1, slot_mib=Non
     recs = [L.gen_json(JSON_BATCH, 42 + rank * 97 + j) for j in range(distinct)]
     hdrs = [W.v2_header(i, 61 + JSON_BATCH) for i in range(n)]
     parts = [list(range(t, n, threads)) for t in range(threads)]
-    prods = [L.Producer(0, slot_bytes=slot_mib << 20, nslots=4, mode=mode) for _ in range(threads)]
+    nslots = int(os.environ.get("RDK_BENCH_PRODUCER_NSLOTS", "4"))
+    prods = [L.Producer(0, slot_bytes=slot_mib << 20, nslots=nslots, mode=mode) for _ in range(threads)]
     out_bytes = [0] * threads
 
     def run(t, todo, count_out):
@@ -1543,9 +1544,13 @@ def main():
             legs["reader_batches_to_rows_1MiB_json"] = leg_line(
                 "reader_batches_to_rows_1MiB_json", rd, LEG_STEPS, 1)
             prod = {}
+            # ring shape per thread count (slot MiB, slots): large slots amortise the block
+            # kernel's fixed latency, a small ring keeps the gather's destination in cache
+            shapes = {1: (128, 8), 2: (128, 8), 4: (64, 2), 8: (32, 2)}
             for th in (1, 2, 4, 8):
-                pr = bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=512), rank, world,
-                                    n=512, threads=th, slot_mib=max(32, 128 // th))
+                os.environ["RDK_BENCH_PRODUCER_NSLOTS"] = str(shapes[th][1])
+                pr = bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=2048), rank, world,
+                                    n=2048, threads=th, slot_mib=shapes[th][0])
                 prod[f"{th}_threads"] = round(pr["bytes"] / (pr["ms"] / 1e3) / 1e9, 2)
                 if th == 1 or prod[f"{th}_threads"] >= max(prod.values()):
                     best = pr

@@ -25,6 +25,8 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <cstdio>
+#include <ctime>
 #include <new>
 #include <vector>
 
@@ -45,7 +47,12 @@ struct Slot {
   hipEvent_t done = nullptr;
   uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
   uint8_t *dh_out = nullptr;  // h_out as seen by the device (the pack kernel writes it)
-  uint8_t *h_meta = nullptr, *d_meta = nullptr;
+  // The batch table lives in mapped pinned memory: the kernels read the few words per batch
+  // that they need, and write their results, straight over PCIe (dh_meta is h_meta as the
+  // device sees it).  Small copies would queue behind the other slots' bulk input copies on
+  // the copy engine and hold this slot's completion back by milliseconds.
+  uint8_t *h_meta = nullptr, *dh_meta = nullptr;
+  unsigned long long *d_cursor = nullptr;  // the pack kernel's output cursor (device atomics)
   size_t in_used = 0, out_used = 0;
   uint32_t nb = 0, polled = 0;
   SlotState st = FREE;
@@ -68,6 +75,8 @@ int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
                               const uint64_t *d_out_offs, uint32_t *d_out_lens, uint32_t n,
                               hipStream_t s, const FuseCrc *fuse);
 bool lz4f_fast_engine_is_units();
+void stage_copy(void *dst, const void *src, size_t n);  // hostcopy.cpp: streaming stores
+void stage_fence();
 
 }  // namespace rdk
 
@@ -80,6 +89,9 @@ struct rdk_hip_producer_s {
   std::vector<Slot> slots;
   int fill = 0;   // slot being filled
   int next = 0;   // oldest slot not fully polled
+  // RDK_HIP_PRODUCER_PROF=1: host nanoseconds spent in the gather, in launch() and in
+  // blocking polls, printed when the producer is destroyed
+  uint64_t ns_gather = 0, ns_launch = 0, ns_wait = 0, n_launch = 0;
 };
 
 namespace {
@@ -251,26 +263,27 @@ RDK_API int rdk_hip_msgset_v2_finalize(const void *d_in, const uint64_t *d_rec_o
 
 namespace {
 
+inline uint64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+const bool g_prof = getenv("RDK_HIP_PRODUCER_PROF") != nullptr;
+
 int launch(rdk_hip_producer_s *p, Slot &sl) {
   const uint32_t B = p->max_batches, n = sl.nb;
-  const Meta hm = meta_at(sl.h_meta, B), dm = meta_at(sl.d_meta, B);
+  stage_fence();  // the gather's streaming stores, before the copy engine reads them
+  const Meta dm = meta_at(sl.dh_meta, B);
   RDK_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, sl.in_used, hipMemcpyHostToDevice, sl.s));
-  RDK_HIP_CHECK(hipMemcpyAsync(dm.rec_offs, hm.rec_offs, size_t(n) * 8, hipMemcpyHostToDevice, sl.s));
-  RDK_HIP_CHECK(hipMemcpyAsync(dm.out_offs, hm.out_offs, size_t(n) * 8, hipMemcpyHostToDevice, sl.s));
-  RDK_HIP_CHECK(hipMemcpyAsync(dm.caps, hm.caps, size_t(n) * 4, hipMemcpyHostToDevice, sl.s));
-  RDK_HIP_CHECK(hipMemcpyAsync(dm.rec_lens, hm.rec_lens, size_t(n) * 4, hipMemcpyHostToDevice, sl.s));
   int rc = rdk_hip_msgset_v2_finalize(sl.d_in, dm.rec_offs, dm.rec_lens, sl.d_out, dm.out_offs,
                                       dm.caps, dm.frame_lens, dm.batch_lens, dm.crcs, n, p->mode,
                                       sl.s);
   if (rc) return rc;
-  RDK_HIP_CHECK(hipMemsetAsync(dm.cursor, 0, 8, sl.s));
+  RDK_HIP_CHECK(hipMemsetAsync(sl.d_cursor, 0, 8, sl.s));
   hipLaunchKernelGGL(pack_to_host_kernel, dim3(n < 2048u ? n : 2048u), dim3(256), 0, sl.s,
                      sl.d_out, dm.out_offs, dm.batch_lens, n, sl.dh_out, dm.pack_offs,
-                     dm.cursor);
+                     sl.d_cursor);
   RDK_HIP_CHECK(hipGetLastError());
-  RDK_HIP_CHECK(hipMemcpyAsync(hm.pack_offs, dm.pack_offs, size_t(n) * 8, hipMemcpyDeviceToHost, sl.s));
-  RDK_HIP_CHECK(hipMemcpyAsync(hm.batch_lens, dm.batch_lens, size_t(n) * 4, hipMemcpyDeviceToHost, sl.s));
-  RDK_HIP_CHECK(hipMemcpyAsync(hm.crcs, dm.crcs, size_t(n) * 4, hipMemcpyDeviceToHost, sl.s));
   RDK_HIP_CHECK(hipEventRecord(sl.done, sl.s));
   sl.st = INFLIGHT;
   sl.polled = 0;
@@ -287,7 +300,7 @@ void release(rdk_hip_producer_s *p) {
     if (sl.h_meta) (void)hipHostFree(sl.h_meta);
     if (sl.d_in) (void)hipFree(sl.d_in);
     if (sl.d_out) (void)hipFree(sl.d_out);
-    if (sl.d_meta) (void)hipFree(sl.d_meta);
+    if (sl.d_cursor) (void)hipFree(sl.d_cursor);
   }
 }
 
@@ -319,10 +332,12 @@ RDK_API rdk_hip_producer_t *rdk_hip_producer_new(int device, size_t slot_bytes, 
         hipHostMalloc(reinterpret_cast<void **>(&sl.h_out), p->out_bytes,
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void **>(&sl.dh_out), sl.h_out, 0) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&sl.h_meta), mb, 0) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&sl.h_meta), mb,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&sl.dh_meta), sl.h_meta, 0) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&sl.d_in), slot_bytes + 256) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&sl.d_out), p->out_bytes) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&sl.d_meta), mb) != hipSuccess) {
+        hipMalloc(reinterpret_cast<void **>(&sl.d_cursor), 8) != hipSuccess) {
       set_error(RDK_HIP_E_NOMEM, "producer: staging allocation failed");
       release(p);
       delete p;
@@ -355,7 +370,9 @@ RDK_API int rdk_hip_producer_produce(rdk_hip_producer_t *p, const void *hdr61, c
   }
   Meta hm = meta_at(sl->h_meta, p->max_batches);
   std::memcpy(sl->h_in + sl->in_used, hdr61, kV2Hdr);
-  if (len) std::memcpy(sl->h_in + sl->in_used + kV2Hdr, records, len);
+  const uint64_t g0 = g_prof ? now_ns() : 0;
+  if (len) stage_copy(sl->h_in + sl->in_used + kV2Hdr, records, len);
+  if (g_prof) p->ns_gather += now_ns() - g0;
   hm.rec_offs[sl->nb] = sl->in_used + kV2Hdr;
   hm.rec_lens[sl->nb] = len;
   hm.out_offs[sl->nb] = sl->out_used;
@@ -371,7 +388,12 @@ RDK_API int rdk_hip_producer_flush(rdk_hip_producer_t *p) {
   if (!p) return set_error(RDK_HIP_E_INVAL, "null producer");
   Slot &sl = p->slots[size_t(p->fill)];
   if (sl.st != FILLING || !sl.nb) return RDK_HIP_OK;
+  const uint64_t l0 = g_prof ? now_ns() : 0;
   int rc = launch(p, sl);
+  if (g_prof) {
+    p->ns_launch += now_ns() - l0;
+    p->n_launch++;
+  }
   if (rc) return rc;
   p->fill = (p->fill + 1) % int(p->slots.size());
   return RDK_HIP_OK;
@@ -385,7 +407,9 @@ RDK_API int rdk_hip_producer_poll(rdk_hip_producer_t *p, rdk_hip_batch_t *out, i
     Slot &sl = p->slots[size_t(p->next)];
     if (sl.st != INFLIGHT) break;
     if (sl.polled == 0) {
+      const uint64_t w0 = g_prof ? now_ns() : 0;
       const hipError_t e = block ? hipEventSynchronize(sl.done) : hipEventQuery(sl.done);
+      if (g_prof) p->ns_wait += now_ns() - w0;
       if (e == hipErrorNotReady) break;
       if (e != hipSuccess)
         return set_error(RDK_HIP_E_HIP, "producer slot: %s", hipGetErrorString(e));
@@ -409,6 +433,9 @@ RDK_API int rdk_hip_producer_poll(rdk_hip_producer_t *p, rdk_hip_batch_t *out, i
 
 RDK_API void rdk_hip_producer_destroy(rdk_hip_producer_t *p) {
   if (!p) return;
+  if (g_prof)
+    fprintf(stderr, "producer %p: gather %.1f ms, launch %.1f ms (%llu launches), blocked in poll %.1f ms\n",
+            (void *)p, p->ns_gather / 1e6, p->ns_launch / 1e6, (unsigned long long)p->n_launch, p->ns_wait / 1e6);
   release(p);
   delete p;
 }

@@ -908,9 +908,11 @@ __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
 // slid down from their slots (raw blocks copied from the input), end mark.
 // FIN: the frame sits 61 bytes into a MsgVersion 2 batch slot and the workgroup also
 // finishes the batch (see FuseCrc): codec choice, header, CRC32C from the block registers.
-constexpr uint32_t kAsmThreads = 1024;  // 16 KiB per read-then-write step of the slide
-
-template <bool FIN>
+// kAsmThreads: threads per workgroup.  1024 (16 KiB per read-then-write step of the slide)
+// when there are few frames; 256 when there are thousands, which are then short: a frame's
+// fixed work is a chain of dependent steps that keeps one workgroup busy for microseconds
+// whatever its size, so what counts is how many frames are in flight per CU.
+template <bool FIN, uint32_t kAsmThreads>
 __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
@@ -1005,10 +1007,16 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
           uint32_t after = 4u;                            // the end mark
           for (uint32_t j = uint32_t(t) + 1u; j < nb; ++j) after += 4u + s_sz[j];
           s_term[t] = crcw_shift(fuse.block_crc[size_t(f) * 64u + uint32_t(t)], after, fuse.x2n);
-        } else if (t == 64) {
+        } else if (t >= 64 && t < 128) {
+          // the second wavefront: header bytes [21, 68) one per lane in a register, then the
+          // byte-table chain over them (no memory access inside the chain)
+          const uint32_t k = 21u + uint32_t(t - 64);
+          const uint32_t hb = ldb(bo + (k < kHdr + 7u ? k : 21u));
           uint32_t r = ~0u;                               // crc32c()'s initial register
-          for (uint32_t k = 21; k < kHdr + 7u; ++k) r = t0[(r ^ ldb(bo + k)) & 0xFFu] ^ (r >> 8);
-          s_term[64] = crcw_shift(r, flen - 7u, fuse.x2n);
+#pragma unroll
+          for (int j = 0; j < int(kHdr + 7u - 21u); ++j)
+            r = t0[(r ^ uint32_t(__builtin_amdgcn_readlane(int(hb), j))) & 0xFFu] ^ (r >> 8);
+          if (t == 64) s_term[64] = crcw_shift(r, flen - 7u, fuse.x2n);
         }
         __syncthreads();
         uint32_t r = s_term[64];
@@ -1069,12 +1077,24 @@ int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
 void lz4f_assemble_launch(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
                           uint32_t n, hipStream_t s, const FuseCrc *fuse) {
-  if (fuse)
-    hipLaunchKernelGGL(lz4f_assemble_kernel<true>, dim3(n < 8192u ? n : 8192u), dim3(kAsmThreads), 0, s,
-                       d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, *fuse);
-  else
-    hipLaunchKernelGGL(lz4f_assemble_kernel<false>, dim3(n < 8192u ? n : 8192u), dim3(kAsmThreads), 0, s,
-                       d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, FuseCrc());
+  const FuseCrc fz = fuse ? *fuse : FuseCrc();
+  if (n > 2048u) {  // thousands of frames: many small workgroups in flight
+    const dim3 grid(n < 32768u ? n : 32768u), block(256);
+    if (fuse)
+      hipLaunchKernelGGL((lz4f_assemble_kernel<true, 256>), grid, block, 0, s, d_in, d_in_offs, d_in_lens,
+                         d_out, d_out_offs, d_out_lens, n, fz);
+    else
+      hipLaunchKernelGGL((lz4f_assemble_kernel<false, 256>), grid, block, 0, s, d_in, d_in_offs, d_in_lens,
+                         d_out, d_out_offs, d_out_lens, n, fz);
+  } else {
+    const dim3 grid(n), block(1024);
+    if (fuse)
+      hipLaunchKernelGGL((lz4f_assemble_kernel<true, 1024>), grid, block, 0, s, d_in, d_in_offs, d_in_lens,
+                         d_out, d_out_offs, d_out_lens, n, fz);
+    else
+      hipLaunchKernelGGL((lz4f_assemble_kernel<false, 1024>), grid, block, 0, s, d_in, d_in_offs, d_in_lens,
+                         d_out, d_out_offs, d_out_lens, n, fz);
+  }
 }
 
 int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,

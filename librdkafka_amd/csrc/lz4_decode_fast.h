@@ -136,9 +136,16 @@ __device__ __forceinline__ void fast_flush(FastDec &d, uint32_t src, uint32_t pc
   // a literal's position is in range of the input only with its tag taken off; a lane
   // without a byte (all ones) stays out of range either way
   d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, src ^ kLitTag, 0, 0);
-  // far history left the ring for memory at least (kRing - kOutChunk) / 64 pieces (that many
-  // vector-memory loads, all waited for) ago: with in-order vmcnt retirement its store has
-  // completed, so no wait is needed
+  // Far history left the ring for memory at least (kRing - kOutChunk) / 64 pieces ago (the
+  // static_assert below keeps that at 32 or more), each of which ended in fast_retire's wait
+  // for its three loads.  The load below relies on two properties of gfx950 that the
+  // language does not promise: vector-memory operations of one wavefront reach the CU's
+  // cache in program order, and vmcnt retires in order, so a store issued before a load
+  // that has since been waited for has itself completed.  The bytes were stored by other
+  // lanes of this same wavefront through this same cache, which a store updates.
+  // tests/test_gpu_lz4.py (matches around the history ring edge) exercises exactly these
+  // sources.
+  static_assert(kRing >= kOutChunk + 2048u, "far history must be at least 32 pieces old");
   d.pfb = d.out[(lit | rk) ? 0u : q];
   asm volatile("" ::: "memory");  // ring bytes stored by other lanes
   d.prb = *ring_at(d, q);

@@ -49,7 +49,17 @@ namespace {
 constexpr int kFastMaxItems = 64;              // block slots per frame per pass
 constexpr uint32_t kFastSlot = kLz4Block + 4;  // worst-case bytes per block in a frame
 constexpr uint32_t kFastHashLog = 12;
-constexpr int kFastLen = 28;                   // match bytes measured from registers
+#ifndef RDK_FAST_PAIRS
+#define RDK_FAST_PAIRS 3
+#endif
+#ifndef RDK_FAST_MAXDIST
+#define RDK_FAST_MAXDIST 65535
+#endif
+constexpr int kFastMaxDist = RDK_FAST_MAXDIST;  // candidates farther back are not looked at
+constexpr int kFastPairs = RDK_FAST_PAIRS;     // dword pairs behind the 4 verified bytes
+constexpr int kFastLen = 4 + 8 * kFastPairs;   // match bytes measured from registers
+constexpr int kWinDwords = 3 + 2 * kFastPairs; // 4 catch-up bytes, the position's dword pair, the pairs
+static_assert(kFastPairs == 2 || kFastPairs == 3, "window loads are written for 7 or 9 dwords");
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
@@ -79,16 +89,35 @@ struct BlockCtx {
 // and its candidate with the candidate's window (Cand, gathered one round
 // ahead).
 struct Win {
-  uint32_t d[9];
+  uint32_t d[kWinDwords];
 };
 struct Cand {
-  uint32_t t[9];
+  uint32_t t[kWinDwords];
   int c;
 };
 
+// kWinDwords dwords at block offset a-4 (a 4-aligned).  Nine dwords: load9.  Seven dwords:
+// two loads, 16 bytes from a-4 and 12 from a+12.  A load that starts below the resource
+// reads as zero as a whole, so a window at a == 0 (the block's first dword) is not usable:
+// win_usable() keeps those positions out of the match search, as position and as candidate
+// (they are still hashed and entered; an entry that points at one is rejected).
+__device__ __forceinline__ void load_win(rsrc_t r, uint32_t a, uint32_t *d) {
+  if constexpr (kWinDwords == 9) {
+    load9(r, a, d);
+  } else {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, a - 4u, 0, 0);
+    const u3 w = __builtin_amdgcn_raw_buffer_load_b96(r, a + 12u, 0, 0);
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    d[4] = w.x; d[5] = w.y; d[6] = w.z;
+  }
+}
+__device__ __forceinline__ bool win_usable(uint32_t a) { return kWinDwords == 9 || a != 0u; }
+
 __device__ __forceinline__ void round_load(const BlockCtx &b, Win &x, int R, int lane) {
   const int i = R + lane;
-  load9(b.r, i <= b.mfl ? ((uint32_t(i) + b.sa) & ~3u) : kNoLoad, x.d);
+  load_win(b.r, i <= b.mfl ? ((uint32_t(i) + b.sa) & ~3u) : kNoLoad, x.d);
 }
 
 // hash + table for the round at R (window x.d arrived), then issue the
@@ -105,8 +134,9 @@ __device__ __forceinline__ void round_lookup(const BlockCtx &b, const Win &x, Ca
   const uint32_t h = hash4(__builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi));
   const int c = act ? int(table[h]) : 0;
   if (act) table[h] = uint16_t(i);
-  y.c = (act && i >= b.p && c < i) ? c : -1;
-  load9(b.r, y.c >= 0 ? ((uint32_t(c) + b.sa) & ~3u) : kNoLoad, y.t);
+  const uint32_t ai = (uint32_t(i) + b.sa) & ~3u, ac = (uint32_t(c) + b.sa) & ~3u;
+  y.c = (act && i >= b.p && c < i && i - c <= kFastMaxDist && win_usable(ai) && win_usable(ac)) ? c : -1;
+  load_win(b.r, y.c >= 0 ? ac : kNoLoad, y.t);
 }
 
 // Write out the queued sequences (lane q < qn holds one: literal start | literal length << 16,
@@ -183,9 +213,9 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
   const uint64_t vm = ballot(valid);
   // first differing bit behind the 4 verified bytes: trailing-zero counts over dword pairs
   // (64 exactly when a pair is equal: only then the next pair counts)
-  uint32_t cz[3];
+  uint32_t cz[kFastPairs];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < kFastPairs; ++k) {
     const uint32_t z0 = __builtin_amdgcn_alignbyte(x.d[2 * k + 3], x.d[2 * k + 2], shi) ^
                         __builtin_amdgcn_alignbyte(y.t[2 * k + 3], y.t[2 * k + 2], shc);
     const uint32_t z1 = __builtin_amdgcn_alignbyte(x.d[2 * k + 4], x.d[2 * k + 3], shi) ^
@@ -193,8 +223,10 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
     const uint64_t w = (uint64_t(z1) << 32) | z0;
     cz[k] = w ? uint32_t(__builtin_ctzll(w)) : 64u;
   }
-  uint32_t fd = cz[1] + (cz[1] >> 6) * cz[2];
-  fd = (cz[0] + (cz[0] >> 6) * fd) >> 3;
+  uint32_t fd = cz[kFastPairs - 1];
+#pragma unroll
+  for (int k = kFastPairs - 2; k >= 0; --k) fd = cz[k] + (cz[k] >> 6) * fd;
+  fd >>= 3;
   int len = 4 + int(fd < uint32_t(kFastLen - 4) ? fd : uint32_t(kFastLen - 4));
   if (len > b.mlim - i) len = b.mlim - i;
 

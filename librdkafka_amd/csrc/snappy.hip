@@ -942,6 +942,12 @@ __device__ __forceinline__ void sn_flush(SnDec &d, uint32_t src, uint32_t pc, ui
   const bool rk = q + kSnRing >= pc;  // a copy source still in the history ring
   // (a lane without a byte stays out of the input's range: positions are below 2^31 - din)
   d.plb = __builtin_amdgcn_raw_buffer_load_b8(d.rin, lit ? q + d.din : kSnNoAccess, 0, 0);
+  // Far history was stored at least (kSnRing - kSnOutChunk) / 64 pieces ago, each of which
+  // ended in sn_retire's wait for its loads.  The load relies on gfx950 handling one
+  // wavefront's vector-memory operations in program order (a store issued before a load that
+  // has been waited for has completed) -- the same reasoning, and the same kind of test
+  // (copies around the ring edge), as in lz4_decode_fast.h.
+  static_assert(kSnRing >= kSnOutChunk + 2048u, "far history must be at least 32 pieces old");
   d.pfb = d.out[(lit | rk) ? 0u : q];
   asm volatile("" ::: "memory");
   d.prb = d.ring[q & kSnRingMask];

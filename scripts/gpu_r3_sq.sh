@@ -6,7 +6,7 @@ TAG="$1"; shift
 R="$GRAFT_REPO_ROOT"
 O="$R/gpurun_out/sq_$TAG"; rm -rf "$O"; mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS -T -f csv -d "$O/pmc" -o t -- python3 $R/bench.py --no-cpu-baseline --no-legs --steps 3 --warmup 1 "$@" > "$O/log" 2>&1 || { echo "SQ_FAILED"; tail -5 "$O/log"; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc ${SQ_COUNTERS:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS} -T -f csv -d "$O/pmc" -o t -- python3 $R/bench.py --no-cpu-baseline --no-legs --steps 3 --warmup 1 "$@" > "$O/log" 2>&1 || { echo "SQ_FAILED"; tail -5 "$O/log"; exit 1; }
 python3 - "$O" <<'PY'
 import csv, glob, sys, collections
 d = sys.argv[1]

@@ -143,6 +143,64 @@ def test_dropin_decompress_block_fuzz_vs_oracle(engine, oracle_mod):
         assert e1 == e2 and o1 == o2, it
 
 
+def _lz4_block(seqs, last):
+    """LZ4 block from (literals, offset, match_length) triples and the last literals."""
+    out = bytearray()
+
+    def ext(v):
+        b = bytearray()
+        v -= 15
+        while v >= 255:
+            b.append(255)
+            v -= 255
+        b.append(v)
+        return b
+
+    for lit, off, ml in seqs:
+        mc = ml - 4
+        out.append((min(len(lit), 15) << 4) | min(mc, 15))
+        if len(lit) >= 15:
+            out += ext(len(lit))
+        out += lit + bytes([off & 0xFF, off >> 8])
+        if mc >= 15:
+            out += ext(mc)
+    out.append(min(len(last), 15) << 4)
+    if len(last) >= 15:
+        out += ext(len(last))
+    return bytes(out + last)
+
+
+def test_decompress_matches_around_the_history_ring_edge(engine, oracle_mod):
+    """Matches whose sources lie just inside and just outside the decoder's on-chip history
+    (4 KiB per wavefront, written out in 1 KiB pieces): offsets 4096 +- a few, offsets that
+    reach back to a piece written moments ago, and sources that straddle the edge.  Each
+    frame is one hand-made block; the oracle decides what it decodes to."""
+    rnd = random.Random(77)
+    for base in (3000, 4096, 5000, 6000, 9000, 20000):
+        first = bytes(rnd.randrange(256) for _ in range(base))
+        seqs = [(first, 1, 4)]
+        pos = base + 4
+        for off in (4090, 4094, 4095, 4096, 4097, 4098, 4100, 4160, 3072, 3071, 3073, 5120, 2048, 1024,
+                    1025, 1023, 8191, 8192, 12000):
+            for ml in (4, 7, 19, 64, 70, 300):
+                if off > pos:
+                    continue
+                lit = bytes(rnd.randrange(256) for _ in range(rnd.choice((0, 1, 3, 17))))
+                seqs.append((lit, off, ml))
+                pos += len(lit) + ml
+                if pos > 60000:
+                    break
+            if pos > 60000:
+                break
+        block = _lz4_block(seqs, bytes(rnd.randrange(256) for _ in range(12)))
+        frame = (bytes([0x04, 0x22, 0x4D, 0x18, 0x60, 0x40, 0x82]) + len(block).to_bytes(4, "little") + block +
+                 bytes(4))
+        e2, want = oracle_mod.rdk_lz4_decompress(frame)
+        assert e2 == 0 and len(want) > base
+        e1, got = engine.rd_kafka_lz4_decompress(1, 0, frame)
+        assert e1 == 0 and got == want, base
+
+
 # ------------------------------------------------------- device batch engine
 def _pack(items, align=64):
     offs, pos = [], 0

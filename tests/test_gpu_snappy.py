@@ -188,6 +188,34 @@ def test_uncompress_element_streams(engine, oracle_mod):
             assert st == engine.SNAPPY_E_IO, (i, st)
 
 
+def test_uncompress_copies_around_the_history_ring_edge(engine, oracle_mod):
+    """copies whose sources lie just inside and just outside the decoder's on-chip history
+    (4 KiB per wavefront, written out in 1 KiB pieces): offsets 4096 +- a few and down to a
+    piece written moments ago; the oracle decides what each stream decodes to"""
+    from snappy_streams import copy, literal, varint
+    rnd = random.Random(78)
+    streams = []
+    for base in (3000, 4096, 5000, 9000, 20000):
+        body = bytearray(literal(rnd, rnd.randbytes(base), False))
+        pos = base
+        for off in (4090, 4094, 4095, 4096, 4097, 4098, 4100, 4160, 3072, 3071, 3073, 5120, 2048, 1024,
+                    1025, 1023, 8191, 8192, 12000):
+            for length in (1, 4, 7, 19, 63, 64):
+                if off > pos:
+                    continue
+                if rnd.random() < 0.5:
+                    lit = rnd.randbytes(rnd.choice((1, 3, 17)))
+                    body += literal(rnd, lit, False)
+                    pos += len(lit)
+                body += copy(rnd, length, off, 2)
+                pos += length
+        streams.append(varint(pos) + bytes(body))
+    want = [oracle_mod.snappy_uncompress(st) for st in streams]
+    assert all(w[0] == 0 for w in want)
+    for i, ((st, out), (err, exp)) in enumerate(zip(_uncompress_batch(engine, streams), want)):
+        assert st == 0 and out == exp, i
+
+
 def test_uncompress_unaligned_destinations(engine, oracle_mod):
     """outputs at every byte alignment with guard bytes between them (single- and
     multi-fragment streams): the bytes arrive and nothing next to them is touched"""

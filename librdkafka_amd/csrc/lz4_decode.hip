@@ -450,10 +450,13 @@ __global__ void lz4f_walk_kernel(const uint8_t *__restrict__ in, const uint64_t 
   }
   wk.fi.nblocks = k < uint32_t(kMaxDesc) ? k : uint32_t(kMaxDesc);
   if ((wk.fi.flags & F_LINKED) || k > uint32_t(kMaxDesc)) wk.fi.flags |= F_SEQ;
-  // Independent blocks decode in place at k * max_block.  A capacity that cannot hold that
-  // layout (a caller that sized the output from what the blocks can yield, for a frame of
-  // many short blocks) is decoded in stream order by one wavefront instead.
-  if (k && uint64_t(k - 1) * wk.fi.max_block + last_most > out_caps[f]) wk.fi.flags |= F_SEQ;
+  // Independent blocks decode in place at k * max_block, each within what is left of the
+  // capacity from there (a frame of full blocks fits a capacity equal to its decoded size).
+  // A capacity that ends before the last block's place -- a caller that sized the output
+  // from what the blocks can yield, for a frame of many short blocks -- cannot hold that
+  // layout: such a frame is decoded in stream order by one wavefront instead.
+  (void)last_most;
+  if (k && uint64_t(k - 1) * wk.fi.max_block >= out_caps[f]) wk.fi.flags |= F_SEQ;
   fs[f].fi = wk.fi;
   fs[f].seq_result = 0;
   if (wk.fi.status == 0 && !(wk.fi.flags & (F_SKIPPABLE | F_SEQ)) && wk.fi.nblocks) {

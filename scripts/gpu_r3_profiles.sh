@@ -13,15 +13,15 @@ run() {
     lz4c) $P lz4f_compress_1MiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload lz4c --partitions 256 --steps 10 ;;
     lz4c_fast) $P lz4f_compress_fast_1MiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload lz4c_fast --partitions 256 --steps 10 ;;
     lz4c_units) $P lz4f_compress_units_1MiB_json "lz4_units_blocks_kernel,lz4f_assemble_kernel" --workload lz4c_units --partitions 256 --steps 10 ;;
-    consumer) $P consumer_crc_verify_lz4f_decompress_1MiB "crc32c_msgset_v2,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_finish_kernel" --workload consumer --partitions 1024 --steps 10 ;;
-    lz4hc9) $P lz4hc_compress_level9_1MiB_json "lz4hc" --workload lz4hc --level 9 --partitions 256 --steps 10 ;;
-    lz4hc12) $P lz4hc_compress_level12_1MiB_json "lz4hc" --workload lz4hc --level 12 --partitions 256 --steps 10 ;;
-    snappyc) $P snappy_compress_1MiB_json "snappy" --workload snappyc --partitions 256 --steps 10 ;;
-    snappyd) $P snappy_uncompress_1MiB_json "snappy" --workload snappyd --partitions 1024 --steps 10 ;;
-    serialize) $P v2_record_serialize_1MiB_json "v2_" --workload serialize --partitions 256 --steps 10 ;;
-    index) $P v2_record_index_1MiB_json "v2_index" --workload index --partitions 256 --steps 10 ;;
-    legacy) $P v1_msgset_crc32_verify_1MiB_json "v01" --workload legacy --partitions 256 --steps 10 ;;
-    perf_tool) $P perf_tool_1M_x_100B_messages "v2_,lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload perf_tool --steps 10 ;;
+    consumer) $P consumer_crc_verify_lz4f_decompress_1MiB "crc32c_msgset_v2,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_seq_kernel,lz4f_finish_kernel" --workload consumer --partitions 1024 --steps 10 ;;
+    lz4hc9) $P lz4hc_compress_level9_1MiB_json "lz4hc_build_kernel,lz4hc_count_items_kernel,lz4hc_compress_blocks_kernel,lz4f_assemble_kernel" --workload lz4hc --level 9 --partitions 256 --steps 10 ;;
+    lz4hc12) $P lz4hc_compress_level12_1MiB_json "lz4hc_build_kernel,lz4hc_count_items_kernel,lz4hc_compress_blocks_kernel,lz4f_assemble_kernel" --workload lz4hc --level 12 --partitions 256 --steps 10 ;;
+    snappyc) $P snappy_compress_1MiB_json "snappy_compress_fragments_kernel,snappy_assemble_kernel" --workload snappyc --partitions 256 --steps 10 ;;
+    snappyd) $P snappy_uncompress_1MiB_json "snappy_scan_kernel,snappy_uncompress_kernel" --workload snappyd --partitions 1024 --steps 10 ;;
+    serialize) $P v2_record_serialize_1MiB_json "v2_batch_kernel,v2_chunk_kernel,v2_fixup_kernel,v2_write_kernel" --workload serialize --partitions 256 --steps 10 ;;
+    index) $P v2_record_index_1MiB_json "v2_index_spec_kernel,v2_index_kernel" --workload index --partitions 256 --steps 10 ;;
+    legacy) $P v1_msgset_crc32_verify_1MiB_json "v01_crc_kernel" --workload legacy --partitions 256 --steps 10 ;;
+    perf_tool) $P perf_tool_1M_x_100B_messages "v2_batch_kernel,v2_chunk_kernel,v2_fixup_kernel,v2_write_kernel,lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload perf_tool --steps 10 ;;
     *) echo "unknown leg $1"; return 1 ;;
   esac
 }

@@ -9,6 +9,15 @@ run() {
     finalize) $P writer_finalize_1MiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload finalize --steps 10 ;;
     finalize_fast_16k) $P writer_finalize_fast_16KiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload finalize_fast --batch-bytes 16384 --partitions 32768 --steps 10 ;;
     finalize_fast_64k) $P writer_finalize_fast_64KiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload finalize_fast --batch-bytes 65536 --partitions 8192 --steps 10 ;;
+    finalize_fast_256k) $P writer_finalize_fast_256KiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload finalize_fast --batch-bytes 262144 --partitions 2048 --steps 10 ;;
+    finalize_16k) $P writer_finalize_16KiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload finalize --batch-bytes 16384 --partitions 32768 --steps 10 ;;
+    finalize_64k) $P writer_finalize_64KiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload finalize --batch-bytes 65536 --partitions 8192 --steps 10 ;;
+    finalize_256k) $P writer_finalize_256KiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload finalize --batch-bytes 262144 --partitions 2048 --steps 10 ;;
+    consumer_16k) $P consumer_crc_verify_lz4f_decompress_16KiB "crc32c_msgset_v2,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_seq_kernel,lz4f_finish_kernel" --workload consumer --batch-bytes 16384 --partitions 32768 --steps 10 ;;
+    consumer_64k) $P consumer_crc_verify_lz4f_decompress_64KiB "crc32c_msgset_v2,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_seq_kernel,lz4f_finish_kernel" --workload consumer --batch-bytes 65536 --partitions 8192 --steps 10 ;;
+    consumer_256k) $P consumer_crc_verify_lz4f_decompress_256KiB "crc32c_msgset_v2,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_seq_kernel,lz4f_finish_kernel" --workload consumer --batch-bytes 262144 --partitions 2048 --steps 10 ;;
+    chain_writer) $P writer_messages_to_batches_1MiB_json "v2_batch_kernel,v2_chunk_kernel,v2_fixup_kernel,v2_write_kernel,lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload chain_writer --partitions 256 --steps 10 ;;
+    chain_reader) $P reader_batches_to_rows_1MiB_json "crc32c_msgset_v2,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_seq_kernel,lz4f_finish_kernel,v2_index_spec_kernel,v2_index_kernel" --workload chain_reader --partitions 256 --steps 10 ;;
     crc) $P crc32c_only_16KiB_batches "crc32c_msgset_v2" --workload crc --steps 10 ;;
     lz4c) $P lz4f_compress_1MiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload lz4c --partitions 256 --steps 10 ;;
     lz4c_fast) $P lz4f_compress_fast_1MiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload lz4c_fast --partitions 256 --steps 10 ;;

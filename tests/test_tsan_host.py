@@ -25,11 +25,18 @@ def driver():
     return BIN
 
 
+@pytest.fixture(scope="module")
+def driver_asan():
+    subprocess.run(["make", "-s", "-C", HERE, "_build/driver_asan"], check=True, timeout=300)
+    return os.path.join(HERE, "_build", "driver_asan")
+
+
 def run(driver, threads, iters, **env):
     p = subprocess.run([driver, str(threads), str(iters)], env=dict(os.environ, **env),
                        capture_output=True, text=True, timeout=600)
     out = p.stdout + p.stderr
-    assert "ThreadSanitizer" not in out, out[-4000:]
+    assert "ThreadSanitizer" not in out and "AddressSanitizer" not in out and "runtime error" not in out, \
+        out[-4000:]
     assert p.returncode == 0, out[-4000:]
     m = re.search(r"bad=(\d+) combined_batches=(\d+) requests=(\d+) largest=(\d+) fallbacks=(\d+) "
                   r"host_crcs=(\d+) ctx=(\d+)/(\d+)", out)
@@ -57,3 +64,11 @@ def test_no_pinned_staging(driver):
 def test_uncombined(driver):
     bad, batches, reqs, largest, fallbacks, host_crcs, made, gone = run(driver, 6, 30, RDK_HIP_COMBINE="0")
     assert bad == 0 and batches == 0 and made == gone
+
+
+def test_address_and_undefined_behaviour_sanitizers(driver_asan):
+    """the same driver under ASan + UBSan with the leak check on: every malloc()ed result is
+    freed by its owner, every context by its thread, on the good path and on the error paths"""
+    for env in ({}, {"STUB_FAIL_EVERY": "5"}, {"STUB_FAIL_ALLOC": "1"}):
+        bad, *_rest, made, gone = run(driver_asan, 6, 30, **env)
+        assert bad == 0 and made == gone

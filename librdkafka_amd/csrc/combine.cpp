@@ -140,6 +140,13 @@ void serve_crc(Ctx *c, Req &r) {
   r.crc = crc_host_segs(r, kind);
 }
 
+// staging for a compress request served alone: the input, and the whole bound when that is
+// small enough for lz4f_compress_host to fetch the frame together with its length
+size_t compress_staging(size_t total) {
+  const size_t bound = lz4f_compress_bound(total);
+  return bound <= (size_t(256) << 10) ? bound : (total ? total : 1);
+}
+
 void keep_error(Req &r) {
   if (r.rc) snprintf(r.err, sizeof r.err, "%s", last_error());
 }
@@ -151,7 +158,8 @@ void serve_one(Ctx *c, Req &r) {
       serve_crc(c, r);
       return;
     case kReqLz4Compress:
-      if ((r.rc = ensure_host(c, r.total ? r.total : 1)) == 0) {
+      // (room for a small frame's bound: it comes back in one copy with its length)
+      if ((r.rc = ensure_host(c, compress_staging(r.total))) == 0) {
         gather(c->h_stage, r);  // the rdkafka_lz4.c:390 loop, gathered
         r.rc = lz4f_compress_host(c, r.total, r.proper_hc, r.level, &r.out, &r.outlen);
       }
@@ -243,8 +251,11 @@ int serve_many(Ctx *c, std::vector<Req *> &batch) {
   const size_t nres = size_t(npieces) + nlz + 2 * size_t(ndz);
   const size_t res_at = n64 * 8 + n32 * 4;
   const size_t desc_bytes = up(res_at + nres * 4, 256);
+  // a small output region comes back whole in the same round trip as the result words; a
+  // large one is fetched frame by frame, at its real length, once the lengths are known
+  const bool whole = out_bytes != 0 && out_bytes <= (size_t(512) << 10);
   int rc;
-  if ((rc = ensure_host(c, desc_bytes + in_bytes)) ||
+  if ((rc = ensure_host(c, desc_bytes + in_bytes + (whole ? out_bytes : 0))) ||
       (rc = ensure_dev(c, 0, desc_bytes + in_bytes + out_bytes + 64)))
     return rc;
   uint8_t *h = c->h_stage, *d = c->d_stage[0];
@@ -327,6 +338,9 @@ int serve_many(Ctx *c, std::vector<Req *> &batch) {
     return rc;
   std::vector<uint32_t> res(nres);
   RDK_HIP_CHECK(hipMemcpyAsync(h + res_at, d_res, nres * 4, hipMemcpyDeviceToHost, s));
+  if (whole)
+    RDK_HIP_CHECK(hipMemcpyAsync(h + desc_bytes + in_bytes, d + desc_bytes + in_bytes, out_bytes,
+                                 hipMemcpyDeviceToHost, s));
   RDK_HIP_CHECK(hipStreamSynchronize(s));
   std::memcpy(res.data(), h + res_at, nres * 4);
   const uint32_t *lz_olen = res.data() + npieces, *dz_olen = lz_olen + nlz;
@@ -339,6 +353,7 @@ int serve_many(Ctx *c, std::vector<Req *> &batch) {
     Req &r = *it.r;
     if (r.kind == kReqLz4Compress) {
       r.outlen = lz_olen[it.first];
+      if (r.outlen > it.out_cap) return set_error(RDK_HIP_E_HIP, "lz4f compress: frame longer than its bound");
     } else if (dz_status[it.first] == kErrDstSizeStatus) {
       return set_error(RDK_HIP_E_HIP, "lz4f decompress: output sizing");
     } else if (dz_status[it.first] != 0) {
@@ -349,7 +364,7 @@ int serve_many(Ctx *c, std::vector<Req *> &batch) {
     }
     back += up(r.outlen, 64);
   }
-  if (back) {
+  if (back && !whole) {
     if ((rc = ensure_host(c, back))) return rc;
     h = c->h_stage;
     size_t at = 0;
@@ -382,7 +397,7 @@ int serve_many(Ctx *c, std::vector<Req *> &batch) {
       r.crc = acc;
       continue;
     }
-    const size_t here = at;
+    const size_t here = whole ? it.out_off : at;  // whole: the device layout, mirrored
     at += up(r.outlen, 64);
     if (r.kind == kReqLz4Decompress && dz_status[it.first] != 0) {
       r.rc = dz_status[it.first];

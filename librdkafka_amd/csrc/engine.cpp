@@ -2,8 +2,10 @@
 //
 // One context per calling thread (librdkafka calls the drop-in symbols from
 // every broker thread concurrently, rdkafka_broker.c:5082): own HIP stream,
-// own pinned staging ring and device scratch, so broker threads never
-// serialise on a shared lock.  CRC tables are uploaded once per device.
+// own pinned staging and device scratch, released when the thread exits.
+// Concurrent drop-in calls are queued and served in batches on the context of
+// whichever caller takes the batch (combine.cpp).  CRC tables are uploaded once
+// per device.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -327,5 +329,5 @@ RDK_API void rdk_hip_ctx_counts(uint64_t out[2]) {
 RDK_API const char *rdk_hip_last_error(void) { return rdk::last_error(); }
 
 RDK_API const char *rdk_hip_version(void) {
-  return "librdkafka_hip 0.4 gfx950 crc32c:group16-bytetab-lds lz4c:window64-exact+round64-fast+fused-crc+seq-queue lz4hc:3-12-lds-build lz4d:seg64-parallel snappy:window64-exact+fragment-decode";
+  return "librdkafka_hip 0.5 gfx950 crc32c:group16-bytetab-lds lz4c:window64-exact+round64-fast+fused-crc+seq-queue+units-lds lz4hc:3-12-lds-build lz4d:seg64-parallel snappy:window64-exact+fragment-decode dropin:combined-callers";
 }

@@ -54,7 +54,7 @@ struct V01 {
   __device__ __forceinline__ bool plausible(const Win &W, uint32_t q) const {
     const uint32_t len = W.len;
     if (q + 34u > W.end) return false;
-    // round 1: Offset, MessageSize, MagicByte/Attributes, KeyLength (v0 at +18, v1 at +26)
+    // first gather: Offset, MessageSize, MagicByte/Attributes, KeyLength (v0 at +18, v1 at +26)
     const uint32_t o1h = W.be32(q), o1l = W.be32(q + 4u), S = W.be32(q + 8u);
     const uint32_t h = W.be32(q + 16u), k0 = W.be32(q + 18u), k1 = W.be32(q + 26u);
     const uint32_t m = h >> 24, a = (h >> 16) & 0xffu, hdr = m ? 14u : 6u;
@@ -66,7 +66,7 @@ struct V01 {
     const uint32_t r = q + 12u + S;
     const bool at_end = r == len;
     ok = ok && (at_end || r + 28u <= W.end);  // the next header must be staged too
-    // round 2: ValueLength, the next message's Offset, MessageSize, MagicByte
+    // second gather: ValueLength, the next message's Offset, MessageSize, MagicByte
     const uint32_t va = ok ? q + 16u + hdr + kb : q, ra = ok && !at_end ? r : q;
     const int32_t vl = int32_t(W.be32(va));
     const uint32_t o2h = W.be32(ra), o2l = W.be32(ra + 4u), S2 = W.be32(ra + 8u);

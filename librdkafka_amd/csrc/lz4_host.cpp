@@ -117,6 +117,9 @@ int lz4f_frame_capacity(const uint8_t *in, size_t inlen, uint64_t *cap_out) {
   return 0;
 }
 
+// frames whose bound is at most this come back in the same copy as their length
+constexpr size_t kOneSyncBytes = 256u << 10;
+
 int lz4f_compress_host(Ctx *c, size_t len, int proper_hc, int level, void **out, size_t *outlen) {
   if (len > 0xFFFFFFFFull) return kErrBadCompression;
   const size_t bound = lz4f_compress_bound(len);
@@ -142,12 +145,20 @@ int lz4f_compress_host(Ctx *c, size_t len, int proper_hc, int level, void **out,
     return rc;
   }
   RDK_HIP_CHECK(hipMemcpyAsync(c->h_desc + 32, d_olen, 4, hipMemcpyDeviceToHost, c->stream));
+  // A small frame comes back whole behind its length, one synchronisation for both (the
+  // staging already has room: the caller sized it for the bound); a large one waits for
+  // its length first and copies only that much.
+  const bool whole = bound <= kOneSyncBytes && c->h_cap >= bound;
+  if (whole) RDK_HIP_CHECK(hipMemcpyAsync(c->h_stage, d_out, bound, hipMemcpyDeviceToHost, c->stream));
   RDK_HIP_CHECK(hipStreamSynchronize(c->stream));
   uint32_t flen;
   std::memcpy(&flen, c->h_desc + 32, 4);
-  if ((rc = ensure_host(c, flen))) return rc;
-  RDK_HIP_CHECK(hipMemcpyAsync(c->h_stage, d_out, flen, hipMemcpyDeviceToHost, c->stream));
-  RDK_HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (flen > bound) return set_error(RDK_HIP_E_HIP, "lz4f compress: frame longer than its bound");
+  if (!whole) {
+    if ((rc = ensure_host(c, flen))) return rc;
+    RDK_HIP_CHECK(hipMemcpyAsync(c->h_stage, d_out, flen, hipMemcpyDeviceToHost, c->stream));
+    RDK_HIP_CHECK(hipStreamSynchronize(c->stream));
+  }
   uint8_t *o = static_cast<uint8_t *>(std::malloc(flen));
   if (!o) return RDK_HIP_RESP_ERR__CRIT_SYS_RESOURCE;
   std::memcpy(o, c->h_stage, flen);
@@ -187,6 +198,9 @@ int lz4f_decompress_host(Ctx *c, int proper_hc, uint8_t *in, size_t inlen, void 
                                    reinterpret_cast<int32_t *>(dw + 3), 1, c->stream)))
     return rc;
   RDK_HIP_CHECK(hipMemcpyAsync(c->h_desc + 64, dw + 2, 8, hipMemcpyDeviceToHost, c->stream));
+  // a small payload comes back whole behind its length and status (one synchronisation)
+  const bool whole = cap != 0 && cap <= kOneSyncBytes;
+  if (whole) RDK_HIP_CHECK(hipMemcpyAsync(c->h_stage, d_out, cap, hipMemcpyDeviceToHost, c->stream));
   RDK_HIP_CHECK(hipStreamSynchronize(c->stream));
   uint32_t olen;
   int32_t status;
@@ -194,7 +208,8 @@ int lz4f_decompress_host(Ctx *c, int proper_hc, uint8_t *in, size_t inlen, void 
   std::memcpy(&status, c->h_desc + 68, 4);
   if (status == kErrDstSize) return set_error(RDK_HIP_E_HIP, "lz4f decompress: output sizing");
   if (status) return status;
-  if (olen) {  // the copy first: nothing is owned yet if it fails
+  if (olen > cap) return set_error(RDK_HIP_E_HIP, "lz4f decompress: length beyond the capacity");
+  if (olen && !whole) {  // the copy first: nothing is owned yet if it fails
     RDK_HIP_CHECK(hipMemcpyAsync(c->h_stage, d_out, olen, hipMemcpyDeviceToHost, c->stream));
     RDK_HIP_CHECK(hipStreamSynchronize(c->stream));
   }

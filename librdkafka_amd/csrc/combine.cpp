@@ -20,7 +20,7 @@
 namespace rdk {
 
 int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
-                      uint32_t *d_scratch, hipStream_t s, int kind);
+                      uint32_t *d_scratch, hipStream_t s, int kind, uint32_t *d_final);
 uint32_t crc_scratch_words(uint64_t len);
 int lz4hc_compress_device(const uint8_t *d_in, const uint64_t *d_in_offs, const uint32_t *d_in_lens,
                           uint8_t *d_out, const uint64_t *d_out_offs, uint32_t *d_out_lens,
@@ -100,10 +100,21 @@ void gather(uint8_t *dst, const Req &r) {
 int crc_staged(Ctx *c, size_t len, uint32_t init, uint32_t *out, int kind) {
   const uint32_t words = crc_scratch_words(len);
   int rc;
-  if ((rc = ensure_dev(c, 0, len + 64)) || (rc = ensure_desc(c, size_t(words) * 4))) return rc;
+  if ((rc = ensure_desc(c, size_t(words) * 4))) return rc;
+  if (c->dh_stage && c->dh_desc) {
+    // the kernels read the mapped staging in place (one pass over PCIe, no copy command to
+    // wait for) and leave the CRC in the mapped result word: launch, synchronise, done
+    if ((rc = crc_device_buffer(c, c->dh_stage, len, init, reinterpret_cast<uint32_t *>(c->d_desc),
+                                c->stream, kind, reinterpret_cast<uint32_t *>(c->dh_desc))))
+      return rc;
+    RDK_HIP_CHECK(hipStreamSynchronize(c->stream));
+    std::memcpy(out, c->h_desc, 4);
+    return 0;
+  }
+  if ((rc = ensure_dev(c, 0, len + 64))) return rc;
   if (len) RDK_HIP_CHECK(hipMemcpyAsync(c->d_stage[0], c->h_stage, len, hipMemcpyHostToDevice, c->stream));
   if ((rc = crc_device_buffer(c, c->d_stage[0], len, init,
-                              reinterpret_cast<uint32_t *>(c->d_desc), c->stream, kind)))
+                              reinterpret_cast<uint32_t *>(c->d_desc), c->stream, kind, nullptr)))
     return rc;
   RDK_HIP_CHECK(hipMemcpyAsync(c->h_desc, c->d_desc + size_t(words - 1) * 4, 4,
                                hipMemcpyDeviceToHost, c->stream));
@@ -258,7 +269,10 @@ int serve_many(Ctx *c, std::vector<Req *> &batch) {
   if ((rc = ensure_host(c, desc_bytes + in_bytes + (whole ? out_bytes : 0))) ||
       (rc = ensure_dev(c, 0, desc_bytes + in_bytes + out_bytes + 64)))
     return rc;
-  uint8_t *h = c->h_stage, *d = c->d_stage[0];
+  // A batch of CRC requests alone never leaves the mapped staging: the ranges kernel reads
+  // descriptors and bytes in place and writes the pieces' CRCs into the result words.
+  const bool in_place = !nlz && !ndz && c->dh_stage != nullptr;
+  uint8_t *h = c->h_stage, *d = in_place ? c->dh_stage : c->d_stage[0];
   uint64_t *h_piece_off = reinterpret_cast<uint64_t *>(h);
   uint64_t *h_lz_in = h_piece_off + npieces, *h_lz_out = h_lz_in + nlz;
   uint64_t *h_dz_in = h_lz_out + nlz, *h_dz_out = h_dz_in + ndz;
@@ -292,7 +306,7 @@ int serve_many(Ctx *c, std::vector<Req *> &batch) {
     out_at += up(size_t(it.out_cap) + 64, 256);
   }
   hipStream_t s = c->stream;
-  RDK_HIP_CHECK(hipMemcpyAsync(d, h, desc_bytes + in_bytes, hipMemcpyHostToDevice, s));
+  if (!in_place) RDK_HIP_CHECK(hipMemcpyAsync(d, h, desc_bytes + in_bytes, hipMemcpyHostToDevice, s));
   const uint64_t *d_piece_off = reinterpret_cast<const uint64_t *>(d);
   const uint64_t *d_lz_in = d_piece_off + npieces, *d_lz_out = d_lz_in + nlz;
   const uint64_t *d_dz_in = d_lz_out + nlz, *d_dz_out = d_dz_in + ndz;
@@ -337,7 +351,7 @@ int serve_many(Ctx *c, std::vector<Req *> &batch) {
                                           d_dz_status, ndz, s)))
     return rc;
   std::vector<uint32_t> res(nres);
-  RDK_HIP_CHECK(hipMemcpyAsync(h + res_at, d_res, nres * 4, hipMemcpyDeviceToHost, s));
+  if (!in_place) RDK_HIP_CHECK(hipMemcpyAsync(h + res_at, d_res, nres * 4, hipMemcpyDeviceToHost, s));
   if (whole)
     RDK_HIP_CHECK(hipMemcpyAsync(h + desc_bytes + in_bytes, d + desc_bytes + in_bytes, out_bytes,
                                  hipMemcpyDeviceToHost, s));

@@ -24,6 +24,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   // pinned host staging (grow-only)
   uint8_t *h_stage = nullptr;
+  uint8_t *dh_stage = nullptr;  // h_stage as the device sees it (nullptr: not mapped)
   size_t h_cap = 0;
   // device scratch (grow-only), independent regions: kScratchStage is the drop-in
   // symbols' staging (only ever used on `stream`, which every drop-in call leaves
@@ -46,6 +47,7 @@ struct Ctx {
   uint8_t *d_desc = nullptr;
   size_t d_desc_cap = 0;
   uint8_t *h_desc = nullptr;  // pinned mirror
+  uint8_t *dh_desc = nullptr; // h_desc as the device sees it (nullptr: not mapped)
 };
 
 // Returns the calling thread's context bound to a device, creating it on

@@ -864,18 +864,23 @@ static void launch_chunks(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t i
 
 // CRC32C of one device buffer (any length) -> d_scratch[nchunks] (device).
 // Used by the drop-in crc32c()/rd_slice_crc32c() after the host gather + H2D.
+// d_final: where the CRC itself goes (default: behind the chunk registers, d_scratch[nchunks]);
+// it may be mapped host memory, which saves the caller a copy.  d_buf may be mapped host
+// memory too: the chunk kernel passes over it once.
 int crc_device_buffer(Ctx *c, const uint8_t *d_buf, uint64_t len, uint32_t init,
-                      uint32_t *d_scratch /* >= nchunks+1 words */, hipStream_t s, int kind) {
+                      uint32_t *d_scratch /* >= nchunks+1 words */, hipStream_t s, int kind,
+                      uint32_t *d_final) {
   const uint32_t nchunks = len ? uint32_t((len + kCrcChunk - 1) / kCrcChunk) : 1u;
+  if (!d_final) d_final = d_scratch + nchunks;
   if (len == 0) {
     // crc32c(crc, buf, 0) == crc: inversions cancel (crc32c.c:102,133)
-    RDK_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_scratch + nchunks), init, 1, s));
+    RDK_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_final), init, 1, s));
     return 0;
   }
   if (crc_variant() != 1) launch_chunks<3>(c, d_buf, len, init, d_scratch, nchunks, s, kind);
   else launch_chunks<1>(c, d_buf, len, init, d_scratch, nchunks, s, kind);
   hipLaunchKernelGGL(crc32c_combine_kernel, dim3(1), dim3(64), 0, s, d_scratch, nchunks, len,
-                     d_scratch + nchunks, crc_x2n_dev(c->device, kind),
+                     d_final, crc_x2n_dev(c->device, kind),
                      kind == kCrcKind32 ? kCrc32Poly : kCrcPoly);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;

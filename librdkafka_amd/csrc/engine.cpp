@@ -198,13 +198,21 @@ int ensure_host(Ctx *c, size_t bytes) {
   size_t n = grow(c->h_cap, bytes);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   c->h_stage = nullptr;
+  c->dh_stage = nullptr;
   c->h_cap = 0;  // a failed allocation must not leave a capacity behind a null pointer
   const size_t lim = scratch_limit();
   if (lim && n > lim)
     return set_error(RDK_HIP_E_NOMEM, "pinned staging of %zu bytes exceeds RDK_HIP_MAX_SCRATCH_BYTES=%zu",
                      n, lim);
-  RDK_HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&c->h_stage), n, hipHostMallocDefault));
+  RDK_HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&c->h_stage), n,
+                              hipHostMallocMapped | hipHostMallocCoherent));
   c->h_cap = n;
+  // the device's view of the staging: kernels that pass over their input once (the CRCs)
+  // read it in place instead of waiting for a copy
+  if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c->dh_stage), c->h_stage, 0) != hipSuccess) {
+    c->dh_stage = nullptr;
+    (void)hipGetLastError();
+  }
   return 0;
 }
 
@@ -299,11 +307,17 @@ int ensure_desc(Ctx *c, size_t bytes) {
   }
   c->d_desc = nullptr;
   c->h_desc = nullptr;
+  c->dh_desc = nullptr;
   c->d_desc_cap = 0;
   size_t n = grow(0, bytes);
   int rc = dev_alloc(&c->d_desc, n);
   if (rc) return rc;
-  RDK_HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&c->h_desc), n, hipHostMallocDefault));
+  RDK_HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&c->h_desc), n,
+                              hipHostMallocMapped | hipHostMallocCoherent));
+  if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c->dh_desc), c->h_desc, 0) != hipSuccess) {
+    c->dh_desc = nullptr;
+    (void)hipGetLastError();
+  }
   c->d_desc_cap = n;
   return 0;
 }

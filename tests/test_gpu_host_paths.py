@@ -51,9 +51,11 @@ def test_thread_context_is_released_at_thread_exit(engine, oracle_mod):
 
 def test_crc_symbols_finish_on_the_host_when_the_device_path_fails(oracle_mod):
     """RDK_HIP_MAX_SCRATCH_BYTES caps pinned staging and device scratch.  Under a 1 MiB cap a
-    just-under-1 MiB crc32c() gets its pinned staging but not its device staging (two failed
-    attempts, then the host finishes from the staged bytes); a 3 MiB one gets neither.  The
-    checksums must be right, the calls counted, and the process must live on."""
+    just-under-1 MiB crc32c() still runs on the device (the CRC kernels read the mapped pinned
+    staging in place, no device staging is needed); a 3 MiB one gets no pinned staging and is
+    finished on the host from the caller's bytes.  The checksums must be right, the calls
+    counted, and the process must live on.  (The retry-then-host path of a failing launch is
+    driven by tests/test_tsan_host.py on the stand-in runtime.)"""
     code = textwrap.dedent("""
         import sys
         sys.path.insert(0, %r)
@@ -64,14 +66,14 @@ def test_crc_symbols_finish_on_the_host_when_the_device_path_fails(oracle_mod):
         assert L.crc32c(0, small) == oracle.crc32c(0, small) and L.dropin_host_crcs() == 0
         a = W.gen_json((1 << 20) - 10, 1)
         assert L.crc32c(7, a) == oracle.crc32c(7, a)
-        assert L.dropin_host_crcs() == 1
+        assert L.dropin_host_crcs() == 0
         b = W.gen_json(3 << 20, 2)
         assert L.crc32c(0, b) == oracle.crc32c(0, b)
         assert L.rd_slice_crc32c([b[:61], b[61:]]) == oracle.crc32c(0, b)
         import zlib
         assert L.rd_slice_crc32([b[:1000], b[1000:]]) == zlib.crc32(b)
-        assert L.dropin_host_crcs() == 4
-        assert L.crc32c(0, small) == oracle.crc32c(0, small) and L.dropin_host_crcs() == 4
+        assert L.dropin_host_crcs() == 3
+        assert L.crc32c(0, small) == oracle.crc32c(0, small) and L.dropin_host_crcs() == 3
         print("survived")
     """ % ROOT)
     env = dict(os.environ, RDK_HIP_MAX_SCRATCH_BYTES=str(1 << 20))

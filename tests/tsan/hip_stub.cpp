@@ -51,6 +51,12 @@ hipError_t hipHostMalloc(void **p, size_t n, unsigned) {
   return *p ? hipSuccess : hipErrorOutOfMemory;
 }
 hipError_t hipHostFree(void *p) { std::free(p); return hipSuccess; }
+hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned) {
+  const char *e = getenv("STUB_NO_MAPPED");  // the copy path instead of the in-place one
+  if (e && atoi(e)) return hipErrorInvalidValue;
+  *d = h;
+  return hipSuccess;
+}
 hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) { std::memcpy(d, s, n); return hipSuccess; }
 hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t) {
   std::memcpy(d, s, n);
@@ -102,9 +108,9 @@ static uint32_t crc_bytes(const uint8_t *p, size_t len, uint32_t init, int kind)
 uint32_t crc_scratch_words(uint64_t) { return 2; }
 
 int crc_device_buffer(Ctx *, const uint8_t *d_buf, uint64_t len, uint32_t init, uint32_t *d_scratch,
-                      hipStream_t, int kind) {
+                      hipStream_t, int kind, uint32_t *d_final) {
   if (entry_fails()) return set_error(RDK_HIP_E_HIP, "stub: crc_device_buffer fails");
-  d_scratch[1] = crc_bytes(d_buf, len, init, kind);
+  *(d_final ? d_final : d_scratch + 1) = crc_bytes(d_buf, len, init, kind);
   return 0;
 }
 

@@ -340,6 +340,48 @@ def test_batch_scale_roundtrip_property(engine):
     assert all(size / 3.2 < int(ol[i]) < size / 2.2 for i in range(4)), ol[:4]
 
 
+def test_thousands_of_multiblock_frames(engine, oracle_mod):
+    """more than 2048 frames of several blocks each (the frame assembler then runs in small
+    workgroups and still has to slide every block down to its place, raw blocks included):
+    a sample of frames byte-identical to the reference's, every frame decoded back"""
+    import numpy as np
+    import torch
+    n = 2300
+    sizes = [150000, 65536, 65537, 200001, 131072, 70000, 13, 0]
+    pieces = [engine.gen_json(sz, 900 + j) if j != 3 else bytes(random.Random(5).randbytes(sz))
+              for j, sz in enumerate(sizes)]  # (j == 3: incompressible, its blocks are stored raw)
+    slot = 200704
+    host = np.zeros(len(sizes) * slot, dtype=np.uint8)
+    for j, p in enumerate(pieces):
+        host[j * slot:j * slot + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    base = torch.from_numpy(host).cuda().view(len(sizes), slot)
+    d_in = torch.empty(n * slot + 256, dtype=torch.uint8, device="cuda")
+    idx = torch.arange(n, device="cuda") % len(sizes)
+    d_in[:n * slot].view(n, slot).copy_(base[idx])
+    in_offs = torch.arange(n, dtype=torch.int64, device="cuda") * slot
+    in_lens = torch.tensor([sizes[i % len(sizes)] for i in range(n)], dtype=torch.int32, device="cuda")
+    bound = (engine.lz4f_compress_bound(max(sizes)) + 255) // 256 * 256
+    d_out = torch.empty(n * bound + 256, dtype=torch.uint8, device="cuda")
+    out_offs = torch.arange(n, dtype=torch.int64, device="cuda") * bound
+    out_lens = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.lz4f_compress_batch(d_in, in_offs, in_lens, d_out, out_offs, out_lens)
+    ol = out_lens.cpu().numpy()
+    want = [oracle_mod.rdk_lz4_compress(p)[1] for p in pieces]
+    for i in list(range(16)) + [777, 1500, n - 3, n - 2, n - 1]:
+        got = bytes(d_out[i * bound:i * bound + int(ol[i])].cpu().numpy())
+        assert got == want[i % len(sizes)], i
+    assert all(int(ol[i]) == len(want[i % len(sizes)]) for i in range(n))
+    d_dec = torch.empty(n * slot + 256, dtype=torch.uint8, device="cuda")
+    caps = torch.full((n,), slot, dtype=torch.int32, device="cuda")
+    dl = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    engine.lz4f_decompress_batch(d_out, out_offs, out_lens, d_dec, in_offs, caps, dl, st)
+    assert int(st.abs().sum()) == 0 and bool((dl == in_lens).all())
+    for j, p in enumerate(pieces):
+        for i in (j, j + 8 * 100, j + 8 * 280):
+            assert bytes(d_dec[i * slot:i * slot + len(p)].cpu().numpy()) == p, i
+
+
 # ------------------------------------------------ throughput-mode compressor
 def _fast_compress(engine, inputs, units=False):
     import torch

@@ -137,3 +137,49 @@ def test_msgset_v2_finalize_device_batches(engine, oracle_mod, mode):
     for i, (hdr, rec) in enumerate(items):
         out = host[out_offs[i]:out_offs[i] + bl[i]]
         _check_batch(oracle_mod, hdr, rec, out, int(cr[i]), "snappy" if mode == 2 else mode == 0)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_msgset_v2_finalize_thousands_of_multiblock_batches(engine, oracle_mod, mode):
+    """more than 2048 MessageSets of several blocks each in one call: the finalizing frame
+    assembler then runs in small workgroups (header, slide, codec choice, CRC terms per block);
+    8 distinct MessageSets rotated, every finished batch compared with the first of its kind
+    and those checked field by field against the oracle, all batches CRC-verified"""
+    import numpy as np
+    import torch
+    rnd = random.Random(90 + mode)
+    sizes = [150000, 65536, 65537, 200001, 131072, 70000, 13, 0]
+    kinds = []
+    for j, n in enumerate(sizes):
+        rec = W.gen_json(n, 300 + j) if j != 3 else rnd.randbytes(n)   # j == 3: kept plain
+        kinds.append((W.v2_header(j, 61 + n), rec))
+    slot = 200704
+    n = 2200
+    host = np.zeros(len(kinds) * slot, dtype=np.uint8)
+    for j, (hdr, rec) in enumerate(kinds):
+        host[j * slot:j * slot + 61] = np.frombuffer(hdr, dtype=np.uint8)
+        host[j * slot + 61:j * slot + 61 + len(rec)] = np.frombuffer(rec, dtype=np.uint8)
+    base = torch.from_numpy(host).cuda().view(len(kinds), slot)
+    d_in = torch.empty(n * slot + 256, dtype=torch.uint8, device="cuda")
+    d_in[:n * slot].view(n, slot).copy_(base[torch.arange(n, device="cuda") % len(kinds)])
+    in_offs = torch.arange(n, dtype=torch.int64, device="cuda") * slot + 61
+    in_lens = torch.tensor([sizes[i % len(sizes)] for i in range(n)], dtype=torch.int32, device="cuda")
+    cap = (61 + engine.lz4f_compress_bound(max(sizes)) + 255) // 256 * 256
+    d_out = torch.zeros(n * cap + 256, dtype=torch.uint8, device="cuda")
+    out_offs = torch.arange(n, dtype=torch.int64, device="cuda") * cap
+    caps = torch.full((n,), cap, dtype=torch.int32, device="cuda")
+    flens, blens, crcs = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    engine.msgset_v2_finalize(d_in, in_offs, in_lens, d_out, out_offs, caps, flens, blens, crcs, mode=mode)
+    bl = blens.cpu().numpy()
+    cr = crcs.cpu().numpy().view(np.uint32)
+    first = []
+    for j, (hdr, rec) in enumerate(kinds):
+        out = bytes(d_out[j * cap:j * cap + int(bl[j])].cpu().numpy())
+        _check_batch(oracle_mod, hdr, rec, out, int(cr[j]), mode == 0)
+        first.append(out)
+    assert all(bl[i] == bl[i % len(kinds)] and cr[i] == cr[i % len(kinds)] for i in range(n))
+    for i in (8, 1001, 2047, 2048, n - 1):
+        assert bytes(d_out[i * cap:i * cap + int(bl[i])].cpu().numpy()) == first[i % len(kinds)], i
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.msgset_v2_crc(d_out, out_offs, caps, st, engine.V2_CRC_VERIFY)
+    assert int(st.abs().sum()) == 0

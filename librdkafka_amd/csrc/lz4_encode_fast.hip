@@ -83,6 +83,8 @@ struct BlockCtx {
   int op;              // output bytes written
   uint32_t q0, q1;     // the sequence queue, one entry per lane (flush_sequences)
   int qn;              // entries queued
+  int rend;            // positions at or past it belong to the next phase: not entered yet
+  int nseq, mbytes;    // sequences and match bytes so far (the stride decision)
 };
 
 // Per round the lane's own 36-byte window (Win, loaded three rounds ahead),
@@ -115,8 +117,13 @@ __device__ __forceinline__ void load_win(rsrc_t r, uint32_t a, uint32_t *d) {
 }
 __device__ __forceinline__ bool win_usable(uint32_t a) { return kWinDwords == 9 || a != 0u; }
 
+// S = stride of the probed positions: lane l of the round at R stands at R + S * l.  With
+// S == 2 every position is still hashed and entered, but only the even ones are looked up,
+// gathered and measured; a match that starts on an odd position is found one byte later
+// and grown back by the catch-up.
+template <int S>
 __device__ __forceinline__ void round_load(const BlockCtx &b, Win &x, int R, int lane) {
-  const int i = R + lane;
+  const int i = R + S * lane;
   load_win(b.r, i <= b.mfl ? ((uint32_t(i) + b.sa) & ~3u) : kNoLoad, x.d);
 }
 
@@ -126,14 +133,22 @@ __device__ __forceinline__ void round_load(const BlockCtx &b, Win &x, int R, int
 // entry the highest lane -- the latest position -- is the one that lands
 // (measured on gfx950; a fixed order either way, so the output is
 // deterministic).
+template <int S>
 __device__ __forceinline__ void round_lookup(const BlockCtx &b, const Win &x, Cand &y, int R,
                                              lds_u16 *table, int lane) {
-  const int i = R + lane;
-  const bool act = i <= b.mfl;
+  const int i = R + S * lane;
+  const bool act = i <= b.mfl && i < b.rend;
   const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
   const uint32_t h = hash4(__builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi));
   const int c = act ? int(table[h]) : 0;
   if (act) table[h] = uint16_t(i);
+  if (S == 2) {  // the odd position behind it: entered, never looked up
+    const bool act1 = i + 1 <= b.mfl && i + 1 < b.rend;
+    const bool wrap = shi == 3u;  // its four bytes start in the next dword
+    const uint32_t lo = wrap ? x.d[2] : x.d[1], hi = wrap ? x.d[3] : x.d[2];
+    const uint32_t h1 = hash4(__builtin_amdgcn_alignbyte(hi, lo, (shi + 1u) & 3u));
+    if (act1) table[h1] = uint16_t(i + 1);
+  }
   const uint32_t ai = (uint32_t(i) + b.sa) & ~3u, ac = (uint32_t(c) + b.sa) & ~3u;
   y.c = (act && i >= b.p && c < i && i - c <= kFastMaxDist && win_usable(ai) && win_usable(ac)) ? c : -1;
   load_win(b.r, y.c >= 0 ? ac : kNoLoad, y.t);
@@ -202,12 +217,18 @@ __device__ __forceinline__ bool flush_sequences(BlockCtx &b, int lane) {
 // sequences together: every chosen lane writes its own token, literals,
 // offset and length bytes at a wave-prefix-sum position.  Returns false when
 // the block does not fit in olimit bytes (stored raw).
+template <int S>
 __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Cand &y, int R,
                                             int lane) {
-  const int i = R + lane;
+  const int i = R + S * lane;
+  const int rel_lane = S * lane;  // this lane's position relative to R
+  // (the parse position is wave-uniform; saying so keeps the walk below on the scalar unit
+  // in every instantiation -- left to the compiler's analysis, the stride-2 one ran it as a
+  // divergent vector loop, 2.5 times the vector instructions per round)
+  const int p0 = __builtin_amdgcn_readfirstlane(b.p);
   const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
   const uint32_t shc = (uint32_t(y.c) + b.sa) & 3u;
-  const bool valid = y.c >= 0 && i >= b.p &&
+  const bool valid = y.c >= 0 && i >= p0 &&
                      __builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi) ==
                          __builtin_amdgcn_alignbyte(y.t[2], y.t[1], shc);
   const uint64_t vm = ballot(valid);
@@ -231,26 +252,30 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
   if (len > b.mlim - i) len = b.mlim - i;
 
   // greedy walk: first verified position at or after the end of the last match
-  const int xin = b.p - R;
+  const int xin = p0 - R;
   int xr = xin;
   uint64_t chosen = 0;
   for (;;) {
     const int rel = xr > 0 ? xr : 0;
-    if (rel >= 64) break;
-    const uint64_t m = vm & (~0ull << rel);
+    const int fl = (rel + S - 1) / S;  // first lane at or past rel
+    if (fl >= 64) break;               // (also keeps the shift below the word's width)
+    const uint64_t m = vm & (~0ull << fl);
     if (!m) break;
     const int q = __builtin_ctzll(m);
     int L = __builtin_amdgcn_readlane(len, q);
-    if (L == kFastLen && R + q + kFastLen < b.mlim) {  // long match: continue from memory
-      const int qi = R + q, off = qi - __builtin_amdgcn_readlane(y.c, q);
+    const int qi = R + S * q;
+    if (L == kFastLen && qi + kFastLen < b.mlim) {  // long match: continue from memory
+      const int off = qi - __builtin_amdgcn_readlane(y.c, q);
       L += wave_count_fwd(b.src + uint32_t(qi + kFastLen), b.src + uint32_t(qi - off + kFastLen),
                           b.mlim - qi - kFastLen, lane);
       if (lane == q) len = L;
     }
     chosen |= 1ull << q;
-    xr = q + L;
+    xr = __builtin_amdgcn_readfirstlane(S * q + L);
+    b.nseq += 1;
+    b.mbytes += L;
   }
-  b.p = chosen ? R + xr : b.p;
+  b.p = chosen ? R + xr : p0;
 
   // sequence fields of the chosen lanes.  Every round runs the same store
   // instructions (parked lanes write nothing), so the vmcnt bookkeeping never
@@ -258,13 +283,13 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
   const bool ch = __builtin_amdgcn_inverse_ballot_w64(chosen);
   const uint64_t below = chosen & ((1ull << lane) - 1ull);
   const int pl = below ? 63 - __builtin_clzll(below) : lane;
-  const int pend = __shfl(lane + len, pl);       // end of the previous chosen match
+  const int pend = __shfl(rel_lane + len, pl);   // end of the previous chosen match
   const int prev = below ? pend : xin;           // this sequence's anchor (relative)
   const uint32_t xb = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi) ^
                       __builtin_amdgcn_alignbyte(y.t[1], y.t[0], shc);
   int bk = xb ? int(__builtin_clz(xb) >> 3) : 4;  // catch-up bytes (lz4.c:957)
-  bk = min(bk, min(lane - prev, y.c));            // literals only, inside the block
-  const uint32_t lit = uint32_t(lane - bk - prev);
+  bk = min(bk, min(rel_lane - prev, y.c));        // literals only, inside the block
+  const uint32_t lit = uint32_t(rel_lane - bk - prev);
   const uint32_t mc = uint32_t(len + bk) - 4u;
   const uint32_t off = uint32_t(i - y.c);
   const uint32_t lstart = uint32_t(R + prev);  // absolute literal start
@@ -288,18 +313,60 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
   return true;
 }
 
-// One pipelined step: the lookup + gather of round R+64 and the window of
-// round R+192 are issued before round R is measured and parsed, so the
-// stores of the previous round's emission never sit between a load and its
-// first use (vmcnt counts loads and stores together).  Every load is issued
-// unconditionally (parked lanes read nothing), so the waits stay exact.
+// One pipelined step: the lookup + gather of the next round and the window of the round
+// three ahead are issued before round R is measured and parsed, so the stores of the previous
+// round's emission never sit between a load and its first use (vmcnt counts loads and stores
+// together).  Every load is issued unconditionally (parked lanes read nothing), so the waits
+// stay exact.
+template <int S>
 __device__ __forceinline__ bool round_step(BlockCtx &b, const Win &cur, Win &next, Win &far,
                                            const Cand &ccur, Cand &cnext, int R, lds_u16 *table,
                                            int lane) {
-  round_lookup(b, next, cnext, R + 64, table, lane);
-  round_load(b, far, R + 192, lane);
-  return round_parse(b, cur, ccur, R, lane);
+  round_lookup<S>(b, next, cnext, R + 64 * S, table, lane);
+  round_load<S>(b, far, R + 192 * S, lane);
+  return round_parse<S>(b, cur, ccur, R, lane);
 }
+
+// The rounds of [r0, b.rend) at stride S (r0 a multiple of 64 * S; positions past mfl are
+// parked).  The pipeline is primed at r0 and drains at the end: positions at or past b.rend
+// are loaded ahead but not entered into the table.  false: the block does not fit.
+template <int S>
+__device__ __forceinline__ bool fast_rounds(BlockCtx &b, lds_u16 *table, int r0, int lane) {
+  constexpr int kSpan = 64 * S;
+  const int last = min(b.mfl, b.rend - 1);  // the last position that starts a round's work
+  if (r0 > last) return true;
+  Win W0, W1, W2, W3;
+  Cand C0, C1;
+  round_load<S>(b, W0, r0, lane);
+  round_load<S>(b, W1, r0 + kSpan, lane);
+  round_load<S>(b, W2, r0 + 2 * kSpan, lane);
+  round_lookup<S>(b, W0, C0, r0, table, lane);
+  for (int R = r0; R <= last; R += 4 * kSpan) {
+    if (!round_step<S>(b, W0, W1, W3, C0, C1, R, table, lane)) return false;
+    if (R + kSpan > last) break;
+    if (!round_step<S>(b, W1, W2, W0, C1, C0, R + kSpan, table, lane)) return false;
+    if (R + 2 * kSpan > last) break;
+    if (!round_step<S>(b, W2, W3, W1, C0, C1, R + 2 * kSpan, table, lane)) return false;
+    if (R + 3 * kSpan > last) break;
+    if (!round_step<S>(b, W3, W0, W2, C1, C0, R + 3 * kSpan, table, lane)) return false;
+  }
+  return true;
+}
+
+// The first kProbe positions of a block are probed one by one; if the matches found there
+// average kStride2MinMatch bytes or more, the rest of the block is probed at every second
+// position.  Long matches survive that unharmed (a match that starts on a skipped position
+// is picked up one byte later and grown back), short ones do not: on text whose matches are
+// 4 to 6 bytes long, probing every second position costs 8 % of the ratio, on the JSON
+// records 2 %, for a third more speed -- so the block's own first matches decide.
+#ifndef RDK_FAST_STRIDE2
+#define RDK_FAST_STRIDE2 1
+#endif
+#ifndef RDK_FAST_PROBE
+#define RDK_FAST_PROBE 2048
+#endif
+constexpr int kProbe = RDK_FAST_PROBE;  // a multiple of 128
+constexpr int kStride2MinMatch = 9;
 
 // Compress one block of n (>= 13) bytes at src into dst (capacity n-1).
 // Returns the compressed size, or 0 when it does not fit (stored raw).
@@ -318,21 +385,19 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
   b.p = b.op = 0;
   b.q0 = b.q1 = 0;
   b.qn = 0;
+  b.nseq = b.mbytes = 0;
 
-  Win W0, W1, W2, W3;
-  Cand C0, C1;
-  round_load(b, W0, 0, lane);
-  round_load(b, W1, 64, lane);
-  round_load(b, W2, 128, lane);
-  round_lookup(b, W0, C0, 0, table, lane);
-  for (int R = 0; R <= b.mfl; R += 256) {
-    if (!round_step(b, W0, W1, W3, C0, C1, R, table, lane)) return 0;
-    if (R + 64 > b.mfl) break;
-    if (!round_step(b, W1, W2, W0, C1, C0, R + 64, table, lane)) return 0;
-    if (R + 128 > b.mfl) break;
-    if (!round_step(b, W2, W3, W1, C0, C1, R + 128, table, lane)) return 0;
-    if (R + 192 > b.mfl) break;
-    if (!round_step(b, W3, W0, W2, C1, C0, R + 192, table, lane)) return 0;
+  b.rend = RDK_FAST_STRIDE2 ? kProbe : n;
+  for (int r0 = 0;;) {  // (a loop so that the one-by-one rounds exist once in the code)
+    if (!fast_rounds<1>(b, table, r0, lane)) return 0;
+    if (b.rend >= n || b.mfl < b.rend) break;
+    r0 = b.rend;
+    b.rend = n;
+    const int nseq = __builtin_amdgcn_readfirstlane(b.nseq);
+    if (nseq > 0 && __builtin_amdgcn_readfirstlane(b.mbytes) >= kStride2MinMatch * nseq) {
+      if (!fast_rounds<2>(b, table, r0, lane)) return 0;
+      break;
+    }
   }
   if (!flush_sequences(b, lane)) return 0;
   // last literals (lz4.c:1141-1166)
@@ -348,7 +413,8 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
   return op + int(last);
 }
 
-__global__ __launch_bounds__(64) void lz4_fast_blocks_kernel(
+// (four waves per SIMD: the measured optimum; the bound also keeps the register count there)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void lz4_fast_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ out_offs, uint32_t n, FuseCrc fuse) {

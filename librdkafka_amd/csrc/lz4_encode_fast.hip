@@ -84,7 +84,8 @@ struct BlockCtx {
   uint32_t q0, q1;     // the sequence queue, one entry per lane (flush_sequences)
   int qn;              // entries queued
   int rend;            // positions at or past it belong to the next phase: not entered yet
-  int nseq, mbytes;    // sequences and match bytes so far (the stride decision)
+  int nseq, mbytes;    // sequences so far; match bytes so far, a partial sum per lane (the stride decision)
+  bool full;           // the block does not fit in olimit bytes: nothing more is written
 };
 
 // Per round the lane's own 36-byte window (Win, loaded three rounds ahead),
@@ -156,8 +157,14 @@ __device__ __forceinline__ void round_lookup(const BlockCtx &b, const Win &x, Ca
 
 // Write out the queued sequences (lane q < qn holds one: literal start | literal length << 16,
 // offset | matchlength-4 << 16): every lane writes its own token, literals, offset and length
-// bytes at a wave-prefix-sum position.  false: the block does not fit in olimit bytes.
-__device__ __forceinline__ bool flush_sequences(BlockCtx &b, int lane) {
+// bytes at a wave-prefix-sum position.  A block that does not fit in olimit bytes sets b.full
+// and writes nothing from then on (the caller stores it raw).
+//
+// The call ends with every load and store of its own retired.  It runs once in several rounds
+// behind a branch; without that wait the compiler has to assume, where the branch joins the
+// round again, that the call's loads may still be pending on registers the round reuses, and
+// drains the round's own loads (the windows and candidates fetched ahead) in every round.
+__device__ __forceinline__ void flush_sequences(BlockCtx &b, int lane) {
   const bool ch = lane < b.qn;
   const uint32_t lstart = b.q0 & 0xFFFFu, lit = ch ? b.q0 >> 16 : 0u;
   const uint32_t off = b.q1 & 0xFFFFu, mc = b.q1 >> 16;
@@ -166,7 +173,12 @@ __device__ __forceinline__ bool flush_sequences(BlockCtx &b, int lane) {
   uint32_t tot;
   const uint32_t o = wave_excl_scan(sz, tot);
   // keep room for the shortest possible last-literals token (lz4.c:1146)
-  if (b.op + int(tot) + 1 > b.olimit) return false;
+  // (wave-uniform, and said to be: the rounds' control flow must stay on the scalar unit)
+  if (__builtin_amdgcn_readfirstlane(int(b.full || b.op + int(tot) + 1 > b.olimit))) {
+    b.full = true;
+    b.qn = 0;
+    return;
+  }
   const uint32_t tp = uint32_t(b.op) + o;  // token position in the block output
   const uint32_t lp = tp + 1u + lext;      // first literal
   const uint32_t fp = lp + lit;            // offset field
@@ -209,16 +221,15 @@ __device__ __forceinline__ bool flush_sequences(BlockCtx &b, int lane) {
   }
   b.op += int(tot);
   b.qn = 0;
-  return true;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 }
 
 // Measure the round's matches (windows arrived), walk the greedy parse over
 // it (scalar: one ctz + one readlane per sequence), then emit the chosen
 // sequences together: every chosen lane writes its own token, literals,
-// offset and length bytes at a wave-prefix-sum position.  Returns false when
-// the block does not fit in olimit bytes (stored raw).
+// offset and length bytes at a wave-prefix-sum position.
 template <int S>
-__device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Cand &y, int R,
+__device__ __forceinline__ void round_parse(BlockCtx &b, const Win &x, const Cand &y, int R,
                                             int lane) {
   const int i = R + S * lane;
   const int rel_lane = S * lane;  // this lane's position relative to R
@@ -251,40 +262,58 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
   int len = 4 + int(fd < uint32_t(kFastLen - 4) ? fd : uint32_t(kFastLen - 4));
   if (len > b.mlim - i) len = b.mlim - i;
 
-  // greedy walk: first verified position at or after the end of the last match
+  // Greedy walk: first verified position at or after the end of the last match.  Every lane
+  // works out its own successor (the first verified lane at or past the end of its match), so
+  // the scalar walk is one readlane per sequence; only a match that fills the register
+  // window is continued from memory, and its successor found from its final length.
+  const int fl = (rel_lane + len + S - 1) / S;  // first lane at or past this lane's match end
+  const uint64_t longm = ballot(valid && len == kFastLen && i + kFastLen < b.mlim);
+  // a lane's successor, as the walk reads it: its lane number, + 64 when that lane holds a
+  // long match (the walk stops there to measure it), 128 when there is none in this round
+  const auto encode = [&](uint64_t ahead, int first) {  // ahead = vm >> first
+    const int t = first + int(__builtin_ctzll(ahead));
+    return ahead ? t + int(((longm >> (t & 63)) & 1ull) << 6) : 128;
+  };
+  const int succ = encode(uint32_t(fl) < 64u ? vm >> fl : 0ull, fl);
   const int xin = p0 - R;
-  int xr = xin;
   uint64_t chosen = 0;
+  const int fl0 = ((xin > 0 ? xin : 0) + S - 1) / S;
+  int q = __builtin_amdgcn_readfirstlane(encode(fl0 < 64 ? vm >> fl0 : 0ull, fl0));
   for (;;) {
-    const int rel = xr > 0 ? xr : 0;
-    const int fl = (rel + S - 1) / S;  // first lane at or past rel
-    if (fl >= 64) break;               // (also keeps the shift below the word's width)
-    const uint64_t m = vm & (~0ull << fl);
-    if (!m) break;
-    const int q = __builtin_ctzll(m);
-    int L = __builtin_amdgcn_readlane(len, q);
-    const int qi = R + S * q;
-    if (L == kFastLen && qi + kFastLen < b.mlim) {  // long match: continue from memory
-      const int off = qi - __builtin_amdgcn_readlane(y.c, q);
-      L += wave_count_fwd(b.src + uint32_t(qi + kFastLen), b.src + uint32_t(qi - off + kFastLen),
-                          b.mlim - qi - kFastLen, lane);
-      if (lane == q) len = L;
+    while (q < 64) {
+      chosen |= 1ull << q;
+      q = __builtin_amdgcn_readlane(succ, q);
     }
+    if (q >= 128) break;
+    q -= 64;  // long match: continue from memory
     chosen |= 1ull << q;
-    xr = __builtin_amdgcn_readfirstlane(S * q + L);
-    b.nseq += 1;
-    b.mbytes += L;
+    const int qi = R + S * q;
+    const int off = qi - __builtin_amdgcn_readlane(y.c, q);
+    const int L = __builtin_amdgcn_readfirstlane(
+        kFastLen + wave_count_fwd(b.src + uint32_t(qi + kFastLen),
+                                  b.src + uint32_t(qi - off + kFastLen),
+                                  b.mlim - qi - kFastLen, lane));
+    if (lane == q) len = L;
+    const int f2 = (S * q + L + S - 1) / S;
+    q = __builtin_amdgcn_readfirstlane(encode(f2 < 64 ? vm >> f2 : 0ull, f2));
   }
+  const int lastq = 63 - int(__builtin_clzll(chosen | 1ull));
+  const int xr = chosen ? S * lastq + __builtin_amdgcn_readlane(len, lastq) : xin;
   b.p = chosen ? R + xr : p0;
 
   // sequence fields of the chosen lanes.  Every round runs the same store
   // instructions (parked lanes write nothing), so the vmcnt bookkeeping never
   // depends on how many sequences a round produced.
   const bool ch = __builtin_amdgcn_inverse_ballot_w64(chosen);
-  const uint64_t below = chosen & ((1ull << lane) - 1ull);
-  const int pl = below ? 63 - __builtin_clzll(below) : lane;
-  const int pend = __shfl(rel_lane + len, pl);   // end of the previous chosen match
-  const int prev = below ? pend : xin;           // this sequence's anchor (relative)
+  if constexpr (S == 1) {  // what the stride decision reads (per-lane partial sums)
+    b.nseq += __builtin_popcountll(chosen);
+    b.mbytes += ch ? len : 0;
+  }
+  // this sequence's anchor (relative): the end of the previous chosen match -- match ends
+  // grow with the lane, so that is the running maximum over the lanes below -- or, for the
+  // round's first sequence, the end of the last round's last match
+  const int pm = wave_excl_max(ch ? rel_lane + len : 0);
+  const int prev = pm > 0 ? pm : xin;
   const uint32_t xb = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi) ^
                       __builtin_amdgcn_alignbyte(y.t[1], y.t[0], shc);
   int bk = xb ? int(__builtin_clz(xb) >> 3) : 4;  // catch-up bytes (lz4.c:957)
@@ -297,7 +326,7 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
   // lane of the queue registers, and written out 64 at a time (flush_sequences).
   const int cnt = __builtin_popcountll(chosen);
   if (cnt) {
-    if (b.qn + cnt > 64 && !flush_sequences(b, lane)) return false;
+    if (b.qn + cnt > 64) flush_sequences(b, lane);
     // chosen lane -> queue lane qn + its rank among the chosen lanes: a forward permute
     // (scatter); the other lanes send to a lane outside the accepted range
     const int rank = int(__builtin_amdgcn_mbcnt_hi(uint32_t(chosen >> 32),
@@ -310,7 +339,6 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
     b.q1 = acc ? r1 : b.q1;
     b.qn += cnt;
   }
-  return true;
 }
 
 // One pipelined step: the lookup + gather of the next round and the window of the round
@@ -319,22 +347,26 @@ __device__ __forceinline__ bool round_parse(BlockCtx &b, const Win &x, const Can
 // together).  Every load is issued unconditionally (parked lanes read nothing), so the waits
 // stay exact.
 template <int S>
-__device__ __forceinline__ bool round_step(BlockCtx &b, const Win &cur, Win &next, Win &far,
+__device__ __forceinline__ void round_step(BlockCtx &b, const Win &cur, Win &next, Win &far,
                                            const Cand &ccur, Cand &cnext, int R, lds_u16 *table,
                                            int lane) {
   round_lookup<S>(b, next, cnext, R + 64 * S, table, lane);
   round_load<S>(b, far, R + 192 * S, lane);
-  return round_parse<S>(b, cur, ccur, R, lane);
+  round_parse<S>(b, cur, ccur, R, lane);
 }
 
 // The rounds of [r0, b.rend) at stride S (r0 a multiple of 64 * S; positions past mfl are
 // parked).  The pipeline is primed at r0 and drains at the end: positions at or past b.rend
-// are loaded ahead but not entered into the table.  false: the block does not fit.
+// are loaded ahead but not entered into the table.  A block that turns out not to fit
+// (b.full) is parsed to its end all the same, writing nothing: such a block has few matches,
+// hence few sequences, and is rarely found out before its last flush anyway, while an exit
+// from inside a round joins the round's path and costs every round a wait for all the loads
+// in flight (the compiler cannot tell at the join which of them the exit left pending).
 template <int S>
-__device__ __forceinline__ bool fast_rounds(BlockCtx &b, lds_u16 *table, int r0, int lane) {
+__device__ __forceinline__ void fast_rounds(BlockCtx &b, lds_u16 *table, int r0, int lane) {
   constexpr int kSpan = 64 * S;
   const int last = min(b.mfl, b.rend - 1);  // the last position that starts a round's work
-  if (r0 > last) return true;
+  if (r0 > last) return;
   Win W0, W1, W2, W3;
   Cand C0, C1;
   round_load<S>(b, W0, r0, lane);
@@ -342,15 +374,14 @@ __device__ __forceinline__ bool fast_rounds(BlockCtx &b, lds_u16 *table, int r0,
   round_load<S>(b, W2, r0 + 2 * kSpan, lane);
   round_lookup<S>(b, W0, C0, r0, table, lane);
   for (int R = r0; R <= last; R += 4 * kSpan) {
-    if (!round_step<S>(b, W0, W1, W3, C0, C1, R, table, lane)) return false;
+    round_step<S>(b, W0, W1, W3, C0, C1, R, table, lane);
     if (R + kSpan > last) break;
-    if (!round_step<S>(b, W1, W2, W0, C1, C0, R + kSpan, table, lane)) return false;
+    round_step<S>(b, W1, W2, W0, C1, C0, R + kSpan, table, lane);
     if (R + 2 * kSpan > last) break;
-    if (!round_step<S>(b, W2, W3, W1, C0, C1, R + 2 * kSpan, table, lane)) return false;
+    round_step<S>(b, W2, W3, W1, C0, C1, R + 2 * kSpan, table, lane);
     if (R + 3 * kSpan > last) break;
-    if (!round_step<S>(b, W3, W0, W2, C1, C0, R + 3 * kSpan, table, lane)) return false;
+    round_step<S>(b, W3, W0, W2, C1, C0, R + 3 * kSpan, table, lane);
   }
-  return true;
 }
 
 // The first kProbe positions of a block are probed one by one; if the matches found there
@@ -386,20 +417,24 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
   b.q0 = b.q1 = 0;
   b.qn = 0;
   b.nseq = b.mbytes = 0;
+  b.full = false;
 
   b.rend = RDK_FAST_STRIDE2 ? kProbe : n;
   for (int r0 = 0;;) {  // (a loop so that the one-by-one rounds exist once in the code)
-    if (!fast_rounds<1>(b, table, r0, lane)) return 0;
-    if (b.rend >= n || b.mfl < b.rend) break;
+    fast_rounds<1>(b, table, r0, lane);
+    if (__builtin_amdgcn_readfirstlane(int(b.full)) || b.rend >= n || b.mfl < b.rend) break;
     r0 = b.rend;
     b.rend = n;
     const int nseq = __builtin_amdgcn_readfirstlane(b.nseq);
-    if (nseq > 0 && __builtin_amdgcn_readfirstlane(b.mbytes) >= kStride2MinMatch * nseq) {
-      if (!fast_rounds<2>(b, table, r0, lane)) return 0;
+    uint32_t mbytes;
+    wave_excl_scan(uint32_t(b.mbytes), mbytes);
+    if (nseq > 0 && int(mbytes) >= kStride2MinMatch * nseq) {
+      fast_rounds<2>(b, table, r0, lane);
       break;
     }
   }
-  if (!flush_sequences(b, lane)) return 0;
+  flush_sequences(b, lane);
+  if (b.full) return 0;
   // last literals (lz4.c:1141-1166)
   const uint32_t last = uint32_t(n - b.p);
   if (b.op + 1 + int(ext_bytes(last)) + int(last) > b.olimit) return 0;

@@ -1,5 +1,5 @@
-"""Regenerate the two number tables of DESIGN.md (drop-in per-call costs, the bench line's legs)
-from profiles/r03/bench_default.json.  usage: python scripts/design_tables.py"""
+"""Regenerate the two number tables of the design document (drop-in per-call costs, the bench
+line's legs) from profiles/r03/bench_default.json.  usage: python scripts/design_tables.py"""
 import json
 import os
 

@@ -81,8 +81,7 @@ struct BlockCtx {
   int n, mfl, mlim, olimit;
   int p;               // parse position == anchor (end of the last match)
   int op;              // output bytes written
-  uint32_t q0, q1;     // the sequence queue, one entry per lane (flush_sequences)
-  int qn;              // entries queued
+  int qn;              // sequences queued in LDS (flush_sequences)
   int rend;            // positions at or past it belong to the next phase: not entered yet
   int nseq, mbytes;    // sequences so far; match bytes so far, a partial sum per lane (the stride decision)
   bool full;           // the block does not fit in olimit bytes: nothing more is written
@@ -96,8 +95,20 @@ struct Win {
 };
 struct Cand {
   uint32_t t[kWinDwords];
-  int c;
+  int c;       // the table's entry for the lane's position
+  uint64_t m;  // lanes whose candidate was gathered (t holds zeros in the others)
 };
+
+// The block's LDS: the hash table, one spare entry that parked lanes read and write (an
+// unconditional LDS access needs no EXEC change, and the code around it stays one basic
+// block that the scheduler can arrange), and the queue of finished sequences.
+constexpr uint32_t kTableEntries = 1u << kFastHashLog;
+typedef uint32_t u32x2q __attribute__((ext_vector_type(2)));  // a queued sequence
+struct __attribute__((aligned(16))) FastLds {
+  uint16_t table[kTableEntries + 8];
+  u32x2q queue[64];
+};
+typedef __attribute__((address_space(3))) u32x2q lds_u2;
 
 // kWinDwords dwords at block offset a-4 (a 4-aligned).  Nine dwords: load9.  Seven dwords:
 // two loads, 16 bytes from a-4 and 12 from a+12.  A load that starts below the resource
@@ -128,34 +139,44 @@ __device__ __forceinline__ void round_load(const BlockCtx &b, Win &x, int R, int
   load_win(b.r, i <= b.mfl ? ((uint32_t(i) + b.sa) & ~3u) : kNoLoad, x.d);
 }
 
-// hash + table for the round at R (window x.d arrived), then issue the
-// candidate gather for the lanes the parse may still need (i >= p).  All 64
-// lanes store their position in one ds_write_b16; where several hit the same
-// entry the highest lane -- the latest position -- is the one that lands
-// (measured on gfx950; a fixed order either way, so the output is
-// deterministic).
+// Lookup, first half: hash + table for the round at R (window x.d arrived).  All 64 lanes
+// store their position in one ds_write_b16; where several hit the same entry the highest
+// lane -- the latest position -- is the one that lands (measured on gfx950; a fixed order
+// either way, so the output is deterministic).  Returns the entry read; the caller uses it
+// only after other work (round_gather), so the LDS round trip is not waited for.
 template <int S>
-__device__ __forceinline__ void round_lookup(const BlockCtx &b, const Win &x, Cand &y, int R,
-                                             lds_u16 *table, int lane) {
+__device__ __forceinline__ int round_lookup(const BlockCtx &b, const Win &x, int R, lds_u16 *table,
+                                            int lane) {
   const int i = R + S * lane;
   const bool act = i <= b.mfl && i < b.rend;
   const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
-  const uint32_t h = hash4(__builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi));
-  const int c = act ? int(table[h]) : 0;
-  if (act) table[h] = uint16_t(i);
+  const uint32_t h = act ? hash4(__builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi)) : kTableEntries;
+  const int c = int(table[h]);
+  table[h] = uint16_t(i);
   if (S == 2) {  // the odd position behind it: entered, never looked up
     const bool act1 = i + 1 <= b.mfl && i + 1 < b.rend;
     const bool wrap = shi == 3u;  // its four bytes start in the next dword
     const uint32_t lo = wrap ? x.d[2] : x.d[1], hi = wrap ? x.d[3] : x.d[2];
-    const uint32_t h1 = hash4(__builtin_amdgcn_alignbyte(hi, lo, (shi + 1u) & 3u));
-    if (act1) table[h1] = uint16_t(i + 1);
+    const uint32_t h1 = act1 ? hash4(__builtin_amdgcn_alignbyte(hi, lo, (shi + 1u) & 3u)) : kTableEntries;
+    table[h1] = uint16_t(i + 1);
   }
-  const uint32_t ai = (uint32_t(i) + b.sa) & ~3u, ac = (uint32_t(c) + b.sa) & ~3u;
-  y.c = (act && i >= b.p && c < i && i - c <= kFastMaxDist && win_usable(ai) && win_usable(ac)) ? c : -1;
-  load_win(b.r, y.c >= 0 ? ac : kNoLoad, y.t);
+  return c;
 }
 
-// Write out the queued sequences (lane q < qn holds one: literal start | literal length << 16,
+// Lookup, second half: issue the candidate gather for the lanes the parse may still need
+// (i >= p).
+template <int S>
+__device__ __forceinline__ void round_gather(const BlockCtx &b, Cand &y, int c, int R, int lane) {
+  const int i = R + S * lane;
+  const uint32_t ai = (uint32_t(i) + b.sa) & ~3u, ac = (uint32_t(c) + b.sa) & ~3u;
+  const bool ok = i <= b.mfl && i < b.rend && i >= b.p && c < i && i - c <= kFastMaxDist &&
+                  win_usable(ai) && win_usable(ac);
+  y.c = c;
+  y.m = ballot(ok);
+  load_win(b.r, ok ? ac : kNoLoad, y.t);
+}
+
+// Write out the queued sequences (entry q < qn: literal start | literal length << 16,
 // offset | matchlength-4 << 16): every lane writes its own token, literals, offset and length
 // bytes at a wave-prefix-sum position.  A block that does not fit in olimit bytes sets b.full
 // and writes nothing from then on (the caller stores it raw).
@@ -164,10 +185,12 @@ __device__ __forceinline__ void round_lookup(const BlockCtx &b, const Win &x, Ca
 // behind a branch; without that wait the compiler has to assume, where the branch joins the
 // round again, that the call's loads may still be pending on registers the round reuses, and
 // drains the round's own loads (the windows and candidates fetched ahead) in every round.
-__device__ __forceinline__ void flush_sequences(BlockCtx &b, int lane) {
+__device__ __forceinline__ void flush_sequences(BlockCtx &b, lds_u2 *queue, int lane) {
   const bool ch = lane < b.qn;
-  const uint32_t lstart = b.q0 & 0xFFFFu, lit = ch ? b.q0 >> 16 : 0u;
-  const uint32_t off = b.q1 & 0xFFFFu, mc = b.q1 >> 16;
+  asm volatile("" ::: "memory");  // (the entries were stored by other lanes)
+  const u32x2q e = queue[lane];
+  const uint32_t lstart = e.x & 0xFFFFu, lit = ch ? e.x >> 16 : 0u;
+  const uint32_t off = e.y & 0xFFFFu, mc = e.y >> 16;
   const uint32_t lext = ext_bytes(lit);
   const uint32_t sz = ch ? 3u + lit + lext + ext_bytes(mc) : 0u;
   uint32_t tot;
@@ -224,25 +247,27 @@ __device__ __forceinline__ void flush_sequences(BlockCtx &b, int lane) {
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 }
 
-// Measure the round's matches (windows arrived), walk the greedy parse over
-// it (scalar: one ctz + one readlane per sequence), then emit the chosen
-// sequences together: every chosen lane writes its own token, literals,
-// offset and length bytes at a wave-prefix-sum position.
+// What round_measure hands to round_walk.
+struct Meas {
+  uint64_t vm;  // lanes with a verified match (MINMATCH bytes equal at a gathered candidate)
+  int len;      // match bytes measured from the register windows, clamped to the block
+  uint32_t shi, shc;
+};
+
+// Measure the round's matches (windows arrived): vector work only.
 template <int S>
-__device__ __forceinline__ void round_parse(BlockCtx &b, const Win &x, const Cand &y, int R,
-                                            int lane) {
+__device__ __forceinline__ Meas round_measure(const BlockCtx &b, const Win &x, const Cand &y, int R,
+                                              int lane) {
   const int i = R + S * lane;
-  const int rel_lane = S * lane;  // this lane's position relative to R
-  // (the parse position is wave-uniform; saying so keeps the walk below on the scalar unit
-  // in every instantiation -- left to the compiler's analysis, the stride-2 one ran it as a
-  // divergent vector loop, 2.5 times the vector instructions per round)
-  const int p0 = __builtin_amdgcn_readfirstlane(b.p);
-  const uint32_t shi = (uint32_t(i) + b.sa) & 3u;
-  const uint32_t shc = (uint32_t(y.c) + b.sa) & 3u;
-  const bool valid = y.c >= 0 && i >= p0 &&
-                     __builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi) ==
-                         __builtin_amdgcn_alignbyte(y.t[2], y.t[1], shc);
-  const uint64_t vm = ballot(valid);
+  Meas m;
+  m.shi = (uint32_t(i) + b.sa) & 3u;
+  m.shc = (uint32_t(y.c) + b.sa) & 3u;
+  const uint32_t shi = m.shi, shc = m.shc;
+  // (positions before the parse position need no exclusion here: the walk starts at it and
+  // only moves forward.  One compare per lane mask: a predicate combined from several goes
+  // through a 0/1 register and a second compare)
+  m.vm = ballot(__builtin_amdgcn_alignbyte(x.d[2], x.d[1], shi) ==
+                __builtin_amdgcn_alignbyte(y.t[2], y.t[1], shc)) & y.m;
   // first differing bit behind the 4 verified bytes: trailing-zero counts over dword pairs
   // (64 exactly when a pair is equal: only then the next pair counts)
   uint32_t cz[kFastPairs];
@@ -259,15 +284,32 @@ __device__ __forceinline__ void round_parse(BlockCtx &b, const Win &x, const Can
 #pragma unroll
   for (int k = kFastPairs - 2; k >= 0; --k) fd = cz[k] + (cz[k] >> 6) * fd;
   fd >>= 3;
-  int len = 4 + int(fd < uint32_t(kFastLen - 4) ? fd : uint32_t(kFastLen - 4));
-  if (len > b.mlim - i) len = b.mlim - i;
+  m.len = 4 + int(fd < uint32_t(kFastLen - 4) ? fd : uint32_t(kFastLen - 4));
+  if (m.len > b.mlim - i) m.len = b.mlim - i;
+  return m;
+}
+
+// Walk the greedy parse over the measured round (scalar: one readlane per sequence), then
+// queue the chosen sequences: every chosen lane stores its sequence's fields at its rank in
+// the LDS queue; flush_sequences writes them out 64 at a time.
+template <int S>
+__device__ __forceinline__ void round_walk(BlockCtx &b, const Win &x, const Cand &y, const Meas &m,
+                                           int R, lds_u2 *queue, int lane) {
+  const int i = R + S * lane;
+  const int rel_lane = S * lane;  // this lane's position relative to R
+  // (the parse position is wave-uniform; saying so keeps the walk below on the scalar unit
+  // in every instantiation -- left to the compiler's analysis, the stride-2 one ran it as a
+  // divergent vector loop, 2.5 times the vector instructions per round)
+  const int p0 = __builtin_amdgcn_readfirstlane(b.p);
+  const uint64_t vm = m.vm;
+  int len = m.len;
 
   // Greedy walk: first verified position at or after the end of the last match.  Every lane
   // works out its own successor (the first verified lane at or past the end of its match), so
   // the scalar walk is one readlane per sequence; only a match that fills the register
   // window is continued from memory, and its successor found from its final length.
   const int fl = (rel_lane + len + S - 1) / S;  // first lane at or past this lane's match end
-  const uint64_t longm = ballot(valid && len == kFastLen && i + kFastLen < b.mlim);
+  const uint64_t longm = vm & ballot(len == kFastLen) & ballot(i + kFastLen < b.mlim);
   // a lane's successor, as the walk reads it: its lane number, + 64 when that lane holds a
   // long match (the walk stops there to measure it), 128 when there is none in this round
   const auto encode = [&](uint64_t ahead, int first) {  // ahead = vm >> first
@@ -297,16 +339,14 @@ __device__ __forceinline__ void round_parse(BlockCtx &b, const Win &x, const Can
     const int f2 = (S * q + L + S - 1) / S;
     q = __builtin_amdgcn_readfirstlane(encode(f2 < 64 ? vm >> f2 : 0ull, f2));
   }
-  const int lastq = 63 - int(__builtin_clzll(chosen | 1ull));
-  const int xr = chosen ? S * lastq + __builtin_amdgcn_readlane(len, lastq) : xin;
-  b.p = chosen ? R + xr : p0;
+  if (!chosen) return;
+  const int lastq = 63 - int(__builtin_clzll(chosen));
+  b.p = R + S * lastq + __builtin_amdgcn_readlane(len, lastq);
 
-  // sequence fields of the chosen lanes.  Every round runs the same store
-  // instructions (parked lanes write nothing), so the vmcnt bookkeeping never
-  // depends on how many sequences a round produced.
   const bool ch = __builtin_amdgcn_inverse_ballot_w64(chosen);
+  const int cnt = __builtin_popcountll(chosen);
   if constexpr (S == 1) {  // what the stride decision reads (per-lane partial sums)
-    b.nseq += __builtin_popcountll(chosen);
+    b.nseq += cnt;
     b.mbytes += ch ? len : 0;
   }
   // this sequence's anchor (relative): the end of the previous chosen match -- match ends
@@ -314,45 +354,37 @@ __device__ __forceinline__ void round_parse(BlockCtx &b, const Win &x, const Can
   // round's first sequence, the end of the last round's last match
   const int pm = wave_excl_max(ch ? rel_lane + len : 0);
   const int prev = pm > 0 ? pm : xin;
-  const uint32_t xb = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], shi) ^
-                      __builtin_amdgcn_alignbyte(y.t[1], y.t[0], shc);
+  const uint32_t xb = __builtin_amdgcn_alignbyte(x.d[1], x.d[0], m.shi) ^
+                      __builtin_amdgcn_alignbyte(y.t[1], y.t[0], m.shc);
   int bk = xb ? int(__builtin_clz(xb) >> 3) : 4;  // catch-up bytes (lz4.c:957)
   bk = min(bk, min(rel_lane - prev, y.c));        // literals only, inside the block
   const uint32_t lit = uint32_t(rel_lane - bk - prev);
   const uint32_t mc = uint32_t(len + bk) - 4u;
   const uint32_t off = uint32_t(i - y.c);
   const uint32_t lstart = uint32_t(R + prev);  // absolute literal start
-  // A round holds a handful of sequences, far fewer than lanes: they are queued, one per
-  // lane of the queue registers, and written out 64 at a time (flush_sequences).
-  const int cnt = __builtin_popcountll(chosen);
-  if (cnt) {
-    if (b.qn + cnt > 64) flush_sequences(b, lane);
-    // chosen lane -> queue lane qn + its rank among the chosen lanes: a forward permute
-    // (scatter); the other lanes send to a lane outside the accepted range
-    const int rank = int(__builtin_amdgcn_mbcnt_hi(uint32_t(chosen >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo(uint32_t(chosen), 0u)));
-    const int tgt = ch ? b.qn + rank : ((b.qn + cnt) & 63);
-    const uint32_t r0 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(lstart | (lit << 16))));
-    const uint32_t r1 = uint32_t(__builtin_amdgcn_ds_permute(tgt << 2, int(off | (mc << 16))));
-    const bool acc = lane >= b.qn && lane < b.qn + cnt;
-    b.q0 = acc ? r0 : b.q0;
-    b.q1 = acc ? r1 : b.q1;
-    b.qn += cnt;
-  }
+  if (b.qn + cnt > 64) flush_sequences(b, queue, lane);
+  const int rank = int(__builtin_amdgcn_mbcnt_hi(uint32_t(chosen >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo(uint32_t(chosen), 0u)));
+  if (ch) queue[b.qn + rank] = u32x2q{lstart | (lit << 16), off | (mc << 16)};
+  b.qn += cnt;
 }
 
-// One pipelined step: the lookup + gather of the next round and the window of the round
-// three ahead are issued before round R is measured and parsed, so the stores of the previous
-// round's emission never sit between a load and its first use (vmcnt counts loads and stores
-// together).  Every load is issued unconditionally (parked lanes read nothing), so the waits
-// stay exact.
+// One pipelined step: the table lookup of the next round and the window of the round three
+// ahead are issued first; round R is measured while the LDS answers; then the next round's
+// candidate gather goes out, and round R is walked and queued.  Every load is issued
+// unconditionally (parked lanes read nothing), so the compiler's waits stay exact, and the
+// stores of a flush never sit between a load and its first use (vmcnt counts loads and
+// stores together).
 template <int S>
 __device__ __forceinline__ void round_step(BlockCtx &b, const Win &cur, Win &next, Win &far,
-                                           const Cand &ccur, Cand &cnext, int R, lds_u16 *table,
+                                           const Cand &ccur, Cand &cnext, int R, FastLds *lds,
                                            int lane) {
-  round_lookup<S>(b, next, cnext, R + 64 * S, table, lane);
+  const int c = round_lookup<S>(b, next, R + 64 * S, (lds_u16 *)lds->table, lane);
   round_load<S>(b, far, R + 192 * S, lane);
-  round_parse<S>(b, cur, ccur, R, lane);
+  const Meas m = round_measure<S>(b, cur, ccur, R, lane);
+  __builtin_amdgcn_sched_barrier(0);  // (the scheduler would pull the gather, and its wait for the LDS, up front)
+  round_gather<S>(b, cnext, c, R + 64 * S, lane);
+  round_walk<S>(b, cur, ccur, m, R, (lds_u2 *)lds->queue, lane);
 }
 
 // The rounds of [r0, b.rend) at stride S (r0 a multiple of 64 * S; positions past mfl are
@@ -363,7 +395,7 @@ __device__ __forceinline__ void round_step(BlockCtx &b, const Win &cur, Win &nex
 // from inside a round joins the round's path and costs every round a wait for all the loads
 // in flight (the compiler cannot tell at the join which of them the exit left pending).
 template <int S>
-__device__ __forceinline__ void fast_rounds(BlockCtx &b, lds_u16 *table, int r0, int lane) {
+__device__ __forceinline__ void fast_rounds(BlockCtx &b, FastLds *lds, int r0, int lane) {
   constexpr int kSpan = 64 * S;
   const int last = min(b.mfl, b.rend - 1);  // the last position that starts a round's work
   if (r0 > last) return;
@@ -372,15 +404,15 @@ __device__ __forceinline__ void fast_rounds(BlockCtx &b, lds_u16 *table, int r0,
   round_load<S>(b, W0, r0, lane);
   round_load<S>(b, W1, r0 + kSpan, lane);
   round_load<S>(b, W2, r0 + 2 * kSpan, lane);
-  round_lookup<S>(b, W0, C0, r0, table, lane);
+  round_gather<S>(b, C0, round_lookup<S>(b, W0, r0, (lds_u16 *)lds->table, lane), r0, lane);
   for (int R = r0; R <= last; R += 4 * kSpan) {
-    round_step<S>(b, W0, W1, W3, C0, C1, R, table, lane);
+    round_step<S>(b, W0, W1, W3, C0, C1, R, lds, lane);
     if (R + kSpan > last) break;
-    round_step<S>(b, W1, W2, W0, C1, C0, R + kSpan, table, lane);
+    round_step<S>(b, W1, W2, W0, C1, C0, R + kSpan, lds, lane);
     if (R + 2 * kSpan > last) break;
-    round_step<S>(b, W2, W3, W1, C0, C1, R + 2 * kSpan, table, lane);
+    round_step<S>(b, W2, W3, W1, C0, C1, R + 2 * kSpan, lds, lane);
     if (R + 3 * kSpan > last) break;
-    round_step<S>(b, W3, W0, W2, C1, C0, R + 3 * kSpan, table, lane);
+    round_step<S>(b, W3, W0, W2, C1, C0, R + 3 * kSpan, lds, lane);
   }
 }
 
@@ -401,7 +433,7 @@ constexpr int kStride2MinMatch = 9;
 
 // Compress one block of n (>= 13) bytes at src into dst (capacity n-1).
 // Returns the compressed size, or 0 when it does not fit (stored raw).
-__device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, int lane) {
+__device__ int fast_block(uintptr_t src, int n, uintptr_t dst, FastLds *lds, int lane) {
   BlockCtx b;
   b.src = src;
   b.dst = dst;
@@ -414,14 +446,13 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
   b.mlim = n - kLz4LastLiterals;  // matchlimit (lz4.c:822)
   b.olimit = n - 1;               // LZ4F_makeBlock dstCapacity
   b.p = b.op = 0;
-  b.q0 = b.q1 = 0;
   b.qn = 0;
   b.nseq = b.mbytes = 0;
   b.full = false;
 
   b.rend = RDK_FAST_STRIDE2 ? kProbe : n;
   for (int r0 = 0;;) {  // (a loop so that the one-by-one rounds exist once in the code)
-    fast_rounds<1>(b, table, r0, lane);
+    fast_rounds<1>(b, lds, r0, lane);
     if (__builtin_amdgcn_readfirstlane(int(b.full)) || b.rend >= n || b.mfl < b.rend) break;
     r0 = b.rend;
     b.rend = n;
@@ -429,11 +460,11 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table, i
     uint32_t mbytes;
     wave_excl_scan(uint32_t(b.mbytes), mbytes);
     if (nseq > 0 && int(mbytes) >= kStride2MinMatch * nseq) {
-      fast_rounds<2>(b, table, r0, lane);
+      fast_rounds<2>(b, lds, r0, lane);
       break;
     }
   }
-  flush_sequences(b, lane);
+  flush_sequences(b, (lds_u2 *)lds->queue, lane);
   if (b.full) return 0;
   // last literals (lz4.c:1141-1166)
   const uint32_t last = uint32_t(n - b.p);
@@ -453,8 +484,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ out_offs, uint32_t n, FuseCrc fuse) {
-  __shared__ __attribute__((aligned(16))) uint16_t table_mem[1u << kFastHashLog];
-  lds_u16 *table = (lds_u16 *)table_mem;
+  __shared__ FastLds lds;
+  uint16_t *table_mem = lds.table;
   const int lane = threadIdx.x;
   const uint64_t items = uint64_t(n) * kFastMaxItems;
   for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
@@ -477,7 +508,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         const u32x4e z = {0u, 0u, 0u, 0u};
         for (int x = lane; x < int((2u << kFastHashLog) / 16u); x += 64) t4[x] = z;
         asm volatile("" ::: "memory");
-        csize = fast_block(src, int(bn), slot + 4u, table, lane);
+        csize = fast_block(src, int(bn), slot + 4u, &lds, lane);
       }
       const uint32_t w = csize ? uint32_t(csize) : (bn | 0x80000000u);  // LZ4F_makeBlock
       if (lane == 0) {

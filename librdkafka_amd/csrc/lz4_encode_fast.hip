@@ -561,7 +561,8 @@ int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
     return lz4f_compress_units_device(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n,
                                       s, fuse);
   const uint64_t items = uint64_t(n) * kFastMaxItems;
-  const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
+  static const unsigned cap = getenv("RDK_HIP_FAST_GRID") ? unsigned(atoi(getenv("RDK_HIP_FAST_GRID"))) : 2560u * 8u;
+  const unsigned grid = unsigned(items < cap ? items : cap);
   hipLaunchKernelGGL(lz4_fast_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
                      d_in_lens, d_out, d_out_offs, n, fuse ? *fuse : FuseCrc());
   lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s, fuse);

@@ -51,6 +51,7 @@
 #include "lz4_device.h"
 #include "lz4_engine.h"
 #include "lz4_wave.h"
+#include "lz4_finish_wave.h"
 #include "win_ring.h"
 
 #ifdef RDK_WIN_PROF
@@ -836,22 +837,6 @@ __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table,
   return op + int(last);
 }
 
-// Raw CRC32C register of one block in stream form (LE32 size word, then the payload the
-// wave has just written or, for a stored block, the source bytes).  The byte table goes
-// into the front of the block's LDS, which is dead once the block is compressed.
-__device__ __forceinline__ uint32_t block_stream_crc(uint32_t w, uintptr_t payload, uint32_t plen,
-                                                     crcw_lds_u32 *t0, const FuseCrc &fuse,
-                                                     int lane) {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the block's own stores are done
-  crcw_load_t0(t0, fuse.t0, lane);
-  uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) r = t0[(r ^ (w >> (8 * j))) & 0xFFu] ^ (r >> 8);
-  const uint32_t c = crcw_shift(r, plen, fuse.x2n) ^ wave_crc_raw(payload, plen, t0, fuse.x2n, lane);
-  asm volatile("" ::: "memory");
-  return c;
-}
-
 // One wavefront per block.  Block k of frame f goes to the worst-case slot
 // at out_offs[f] + 7 + k*kSlot as [LE32 size word][payload]; a block stored
 // raw gets only its size word (payload is taken from the input later).
@@ -859,7 +844,8 @@ template <bool WINDOWS>
 __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
-    const uint64_t *__restrict__ out_offs, uint32_t n, int accel, FuseCrc fuse) {
+    const uint64_t *__restrict__ out_offs, uint32_t *__restrict__ out_lens, uint32_t n, int accel,
+    FuseCrc fuse) {
   // the source ring (windowed engine) sits in front of the hash table
   constexpr uint32_t kRingLds = WINDOWS ? kRingBytes : 0u;
   __shared__ __attribute__((aligned(16))) uint8_t lds_mem[kRingLds + (2u << kHashLog)];
@@ -896,10 +882,14 @@ __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
         stb(slot, w & 0xFFu); stb(slot + 1, (w >> 8) & 0xFFu);
         stb(slot + 2, (w >> 16) & 0xFFu); stb(slot + 3, w >> 24);
       }
-      if (fuse.block_crc && k < uint32_t(kEncMaxItems))
-        fuse.block_crc[size_t(f) * kEncMaxItems + k] =
-            block_stream_crc(w, csize ? slot + 4u : src, csize ? uint32_t(csize) : bn,
-                             (crcw_lds_u32 *)lds_mem, fuse, lane);
+      if (fuse.block_crc && k < uint32_t(kEncMaxItems)) {
+        // the compress epilogue's CRC (lz4_finish_wave.h); the byte tables go into the front
+        // of the block's LDS, which is dead once the block is compressed
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the block's own stores are done
+        wave_block_epilogue(uni(w), slot, src, k, nb, f, reinterpret_cast<uintptr_t>(out) + out_offs[f],
+                            reinterpret_cast<uintptr_t>(in) + in_offs[f], len, out_lens, fuse,
+                            (crcw_lds_u32 *)lds_mem, lane);
+      }
     }
   }
 }
@@ -987,6 +977,7 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
   for (uint32_t f = blockIdx.x; f < n; f += gridDim.x) {
     const uint32_t len = in_lens[f];
     const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
+    if (FIN && fuse.single_done && nb == 1u) continue;  // finished by the block kernel's wave
     const uintptr_t ob = reinterpret_cast<uintptr_t>(out) + out_offs[f];
     const uintptr_t ib = reinterpret_cast<uintptr_t>(in) + in_offs[f];
     if (t == 0) {  // magic, FLG 0x60 (v01, independent), BD 0x40 (64 KB), HC 0x82
@@ -1100,7 +1091,8 @@ int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
                          const FuseCrc *fuse) {
   (void)c;
   if (!n) return 0;
-  const FuseCrc fz = fuse ? *fuse : FuseCrc();
+  FuseCrc fz = fuse ? *fuse : FuseCrc();
+  fz.single_done = fz.block_crc != nullptr;
   uint64_t items = uint64_t(n) * kEncMaxItems;
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
   // RDK_HIP_LZ4_EXACT_SEQ=1 keeps the sequence-at-a-time engine for acceleration 1 too
@@ -1108,11 +1100,12 @@ int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
   static const bool seq_only = getenv("RDK_HIP_LZ4_EXACT_SEQ") && atoi(getenv("RDK_HIP_LZ4_EXACT_SEQ"));
   if (accel == 1 && !seq_only)
     hipLaunchKernelGGL(lz4_compress_blocks_kernel<true>, dim3(grid), dim3(64), 0, s, d_in,
-                       d_in_offs, d_in_lens, d_out, d_out_offs, n, accel, fz);
+                       d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, accel, fz);
   else
     hipLaunchKernelGGL(lz4_compress_blocks_kernel<false>, dim3(grid), dim3(64), 0, s, d_in,
-                       d_in_offs, d_in_lens, d_out, d_out_offs, n, accel, fz);
-  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s, fuse);
+                       d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, accel, fz);
+  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s,
+                       fuse ? &fz : nullptr);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;
 }

@@ -34,6 +34,7 @@
 
 #include "common.h"
 #include "crc_wave.h"
+#include "lz4_finish_wave.h"
 #include "lz4_device.h"
 #include "lz4_engine.h"
 #include "lz4_wave.h"
@@ -483,7 +484,8 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, FastLds *lds, int
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void lz4_fast_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
     const uint32_t *__restrict__ in_lens, uint8_t *__restrict__ out,
-    const uint64_t *__restrict__ out_offs, uint32_t n, FuseCrc fuse) {
+    const uint64_t *__restrict__ out_offs, uint32_t *__restrict__ out_lens, uint32_t n,
+    FuseCrc fuse) {
   __shared__ FastLds lds;
   uint16_t *table_mem = lds.table;
   const int lane = threadIdx.x;
@@ -516,19 +518,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         stb(slot + 2, (w >> 16) & 0xFFu); stb(slot + 3, w >> 24);
       }
       if (fuse.block_crc && k < uint32_t(kFastMaxItems)) {
-        // the compress epilogue's CRC (crc_wave.h): raw register of the block in stream
-        // form; the byte table goes into the hash table's LDS, dead until the next block
+        // the compress epilogue's CRC (lz4_finish_wave.h); the byte tables go into the hash
+        // table's LDS, dead until the next block
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        crcw_lds_u32 *t0 = (crcw_lds_u32 *)table_mem;
-        crcw_load_t0(t0, fuse.t0, lane);
-        uint32_t r = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) r = t0[(r ^ (w >> (8 * j))) & 0xFFu] ^ (r >> 8);
-        const uint32_t plen = csize ? uint32_t(csize) : bn;
-        fuse.block_crc[size_t(f) * kFastMaxItems + k] =
-            crcw_shift(r, plen, fuse.x2n) ^
-            wave_crc_raw(csize ? slot + 4u : src, plen, t0, fuse.x2n, lane);
-        asm volatile("" ::: "memory");
+        wave_block_epilogue(uni(w), slot, src, k, nb, f, reinterpret_cast<uintptr_t>(out) + out_offs[f],
+                            reinterpret_cast<uintptr_t>(in) + in_offs[f], len, out_lens, fuse,
+                            (crcw_lds_u32 *)table_mem, lane);
       }
     }
   }
@@ -561,11 +556,13 @@ int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
     return lz4f_compress_units_device(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n,
                                       s, fuse);
   const uint64_t items = uint64_t(n) * kFastMaxItems;
-  static const unsigned cap = getenv("RDK_HIP_FAST_GRID") ? unsigned(atoi(getenv("RDK_HIP_FAST_GRID"))) : 2560u * 8u;
-  const unsigned grid = unsigned(items < cap ? items : cap);
+  const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
+  FuseCrc fz = fuse ? *fuse : FuseCrc();
+  fz.single_done = fz.block_crc != nullptr;
   hipLaunchKernelGGL(lz4_fast_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
-                     d_in_lens, d_out, d_out_offs, n, fuse ? *fuse : FuseCrc());
-  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s, fuse);
+                     d_in_lens, d_out, d_out_offs, d_out_lens, n, fz);
+  lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s,
+                       fuse ? &fz : nullptr);
   RDK_HIP_CHECK(hipGetLastError());
   return 0;
 }

@@ -31,6 +31,9 @@ struct FuseCrc {
   const uint32_t *x2n = nullptr;   // x^(2^k) mod P, k = 0..63 (device)
   uint32_t *batch_lens = nullptr;  // out: 61 + payload bytes
   uint32_t *crcs = nullptr;        // out: the stored CRC
+  // Set by an engine whose block kernel finishes the batches of single-block frames itself
+  // (lz4_finish_wave.h); the assembler then passes over them.
+  bool single_done = false;
 };
 
 }  // namespace rdk

@@ -183,3 +183,70 @@ def test_msgset_v2_finalize_thousands_of_multiblock_batches(engine, oracle_mod, 
     st = torch.zeros(n, dtype=torch.int32, device="cuda")
     engine.msgset_v2_crc(d_out, out_offs, caps, st, engine.V2_CRC_VERIFY)
     assert int(st.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_msgset_v2_finalize_single_block_batches(engine, oracle_mod, mode):
+    """MessageSets of at most one 64 KiB block are finished by the wavefront that compressed
+    them (no assembler pass): sizes around every boundary of that path -- shorter than the
+    shortest compressible block, around the 16-byte pieces and 4-byte words of the in-wave
+    CRC, the full block -- compressible and not (kept plain), at every input alignment;
+    every field, the frame length and the CRC against the oracle."""
+    import numpy as np
+    import torch
+    rnd = random.Random(120 + mode)
+    sizes = list(range(1, 70)) + [100, 255, 256, 257, 1000, 1023, 1024, 1025, 4095, 4096, 4097, 16384,
+                                  20000, 65519, 65520, 65521, 65535, 65536]
+    sizes += [rnd.randrange(1, 65537) for _ in range(60)]
+    items = []
+    for i, n in enumerate(sizes):
+        kind = i % 5
+        if kind == 0:
+            rec = rnd.randbytes(n)                       # kept plain
+        elif kind == 1:
+            rec = (rnd.randbytes(7) * (n // 7 + 1))[:n]  # long matches
+        elif kind == 2:
+            rec = bytes(n)
+        else:
+            rec = W.gen_json(n, 500 + i)
+        hdr = bytearray(W.v2_header(i, 61 + n))
+        hdr[21:23] = (0x10 if i % 3 == 0 else 0).to_bytes(2, "big")
+        items.append((bytes(hdr), rec))
+    in_offs, pos = [], 0
+    for i, (hdr, rec) in enumerate(items):
+        pos += i % 4                                     # every alignment of the records
+        in_offs.append(pos + 61)
+        pos += 61 + len(rec)
+    hbuf = bytearray(pos + 256)
+    for o, (hdr, rec) in zip(in_offs, items):
+        hbuf[o - 61:o] = hdr
+        hbuf[o:o + len(rec)] = rec
+    caps = [61 + engine.lz4f_compress_bound(len(rec)) + (i * 7) % 13 for i, (_, rec) in enumerate(items)]
+    out_offs = np.concatenate([[0], np.cumsum(caps)[:-1]])
+    n = len(items)
+    d_in = torch.frombuffer(hbuf, dtype=torch.uint8).cuda()
+    d_out = torch.zeros(int(sum(caps)) + 256, dtype=torch.uint8, device="cuda")
+    t64 = lambda a: torch.tensor(np.asarray(a, dtype=np.int64), device="cuda")  # noqa: E731
+    t32 = lambda a: torch.tensor(np.asarray(a, dtype=np.int32), device="cuda")  # noqa: E731
+    flens, blens, crcs = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    engine.msgset_v2_finalize(d_in, t64(in_offs), t32([len(r) for _, r in items]), d_out,
+                              t64(out_offs), t32(caps), flens, blens, crcs, mode=mode)
+    host = bytes(d_out.cpu().numpy())
+    bl = blens.cpu().numpy()
+    fl = flens.cpu().numpy()
+    cr = crcs.cpu().numpy().view(np.uint32)
+    plain = 0
+    for i, (hdr, rec) in enumerate(items):
+        out = host[out_offs[i]:out_offs[i] + bl[i]]
+        _check_batch(oracle_mod, hdr, rec, out, int(cr[i]), mode == 0)
+        if int.from_bytes(out[21:23], "big") & 7 == 3:
+            assert fl[i] == bl[i] - 61, i
+        else:
+            plain += 1
+            assert fl[i] > len(rec), i                   # the frame that was not kept
+        if mode == 0:
+            assert fl[i] == len(oracle_mod.rdk_lz4_compress(rec)[1]), i
+    assert plain >= n // 5
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.msgset_v2_crc(d_out, t64(out_offs), t32(caps), st, engine.V2_CRC_VERIFY)
+    assert int(st.abs().sum()) == 0

@@ -6,22 +6,24 @@
 // match search is restructured for a wavefront instead of emulating the
 // sequential LZ4_compress_generic loop (lz4.c:789-1177) step by step:
 //
-//   * positions are processed in rounds of 64 (one per lane).  Every position
-//     <= n-12 is hashed with LZ4_hash4 (lz4.c:631) into a 2^13-entry u16 table
-//     in LDS that holds the LATEST earlier position per hash (dense insertion,
-//     the reference inserts only the positions it probes);
-//   * a lane's candidate is the table entry as of the start of its round; the
-//     lane verifies MINMATCH bytes, measures up to 16 match bytes and up to 4
-//     catch-up bytes (lz4.c:957) from two 24-byte register windows (its own
-//     position and the candidate's), so one round costs two gathers, not a
-//     chain of dependent loads per sequence;
-//   * the greedy parse (first verified position at or after the end of the
-//     previous match) is scalar: a ctz over the round's match ballot and one
-//     readlane per sequence; only matches longer than 16 bytes go back to
-//     memory (64 bytes per wave step);
-//   * sequences are collected 64 at a time in two VGPRs and emitted together:
-//     a wave prefix sum places every sequence, each lane writes its token,
-//     length bytes, literals and offset (LZ4 block format, lz4.c:961-1073).
+//   * positions are processed in rounds of 64 probes (one per lane).  Every position
+//     <= n-12 is hashed with LZ4_hash4 (lz4.c:631) into a 2^12-entry u16 table in LDS that
+//     holds the LATEST earlier position per hash (dense insertion, the reference inserts
+//     only the positions it probes);
+//   * a lane's candidate is the table entry as of the start of its round; the lane verifies
+//     MINMATCH bytes, measures up to 28 match bytes and up to 4 catch-up bytes (lz4.c:957)
+//     from two 36-byte register windows (its own position's, loaded three rounds ahead, and
+//     the candidate's, gathered one round ahead), so a round costs two gathers, not a chain
+//     of dependent loads per sequence;
+//   * the greedy parse (first verified position at or after the end of the previous match)
+//     is a scalar walk of one readlane per sequence over successors that every lane has
+//     worked out for itself; only matches longer than 28 bytes go back to memory (64 bytes
+//     per wave step);
+//   * a block whose first 2 KiB match well is probed at every second position from there on
+//     (every position is still entered into the table);
+//   * sequences are queued in LDS and emitted 64 at a time: a wave prefix sum places every
+//     sequence, each lane writes its token, length bytes, literals and offset (LZ4 block
+//     format, lz4.c:961-1073).
 //
 // The output is a valid LZ4 frame that the reference decoder
 // (rd_kafka_lz4_decompress, rdkafka_lz4.c:167) decodes to the input; it is NOT

@@ -140,6 +140,14 @@ void crc_build_x2n(uint32_t *out, uint32_t poly) {
   for (int k = 1; k < 64; ++k) out[k] = p = crc_multmodp(p, p, poly);
 }
 
+void crc_build_x2n_dev(uint32_t *out, uint32_t poly) {
+  crc_build_x2n(out, poly);
+  uint32_t p = 1u << 31;  // x^0
+  for (int i = 0; i < kXLoN; ++i, p = crc_multmodp(p, out[3], poly)) out[kXLo + i] = p;        // * x^8
+  p = 1u << 31;
+  for (int i = 0; i < kXHiN; ++i, p = crc_multmodp(p, out[13], poly)) out[kXHi + i] = p;       // * x^(8 * 1024)
+}
+
 // x^(8 * nbytes) mod P from the x2n table (bit k of the bit count selects x2n[k])
 uint32_t crc_x_pow_bytes(const uint32_t x2n[64], uint64_t nbytes, uint32_t poly) {
   uint32_t p = 1u << 31;  // x^0

@@ -59,6 +59,14 @@ constexpr int kLaneStride = 1024;               // bytes between a lane's vector
 constexpr int v3_byte_table(int i) { return i < 16 ? i * 2048 + 1024 : kV3ByteHi + (i - 16) * 1024; }
 void crc_build_tables_v3(uint32_t *out /* kCrcV3Words */, uint32_t poly = kCrcPoly);
 void crc_build_x2n(uint32_t *out /* 64 */, uint32_t poly = kCrcPoly);
+// The device copy of the x2n table carries two more tables behind its 64 words, so that a
+// kernel finds x^(8n) for a byte count n < 4 MiB with two loads and one multiplication
+// instead of one multiplication per set bit of n:
+//   [kXLo + i]  = x^(8 * i),         i < kXLoN
+//   [kXHi + i]  = x^(8 * kXLoN * i), i < kXHiN
+constexpr int kXLo = 64, kXLoN = 1024, kXHi = kXLo + kXLoN, kXHiN = 4096;
+constexpr int kX2nDevWords = kXHi + kXHiN;
+void crc_build_x2n_dev(uint32_t *out /* kX2nDevWords */, uint32_t poly = kCrcPoly);
 
 // ---- v4 image (batched ranges / MsgVersion 2 kernels): 16-lane groups, byte tables
 // A 16-lane group CRCs one range.  Per step the group reads kV4Vecs x 256 contiguous bytes:

@@ -46,6 +46,17 @@ __device__ __forceinline__ uint32_t crcw_shift(uint32_t r, uint32_t nbytes,
   return nbytes ? crcw_mul(crcw_xpow8n(nbytes, x2n), r) : r;
 }
 
+// The same with the power looked up (x2n is the device table, whose two byte-power tables
+// follow the 64 squarings, crc32c_tables.h): two loads and two multiplications for any count
+// below 4 MiB, where the loop above multiplies once per set bit of the count.
+__device__ __forceinline__ uint32_t crcw_shift_lut(uint32_t r, uint32_t nbytes,
+                                                   const uint32_t *__restrict__ x2n) {
+  static_assert(kXLoN == 1024, "the split below is at bit 10");
+  if (nbytes >= uint32_t(kXLoN) * uint32_t(kXHiN)) return crcw_shift(r, nbytes, x2n);
+  const uint32_t lo = x2n[kXLo + (nbytes & uint32_t(kXLoN - 1))], hi = x2n[kXHi + (nbytes >> 10)];
+  return crcw_mul(crcw_mul(lo, hi), r);
+}
+
 // 256 dwords of the byte table T0 (raw CRC of one byte) into LDS, by one wave
 __device__ __forceinline__ void crcw_load_t0(crcw_lds_u32 *t0, const uint32_t *__restrict__ tabs,
                                              int lane) {

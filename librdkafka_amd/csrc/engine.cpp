@@ -106,13 +106,13 @@ int upload_tables(int dev) {
   static uint32_t host_tab[kCrcTableWords];
   static uint32_t host_tab2[kCrcV3Words];
   static uint32_t host_tab4[kCrcV4Words];
-  static uint32_t host_x2n[64];
+  static uint32_t host_x2n[kX2nDevWords];
   for (int kind = 0; kind < 2; ++kind) {
     const uint32_t poly = kind ? kCrc32Poly : kCrcPoly;
     crc_build_tables(host_tab, poly);
     crc_build_tables_v4(host_tab4, poly);
     crc_build_tables_v3(host_tab2, poly);
-    crc_build_x2n(host_x2n, poly);
+    crc_build_x2n_dev(host_x2n, poly);
     int rc;
     if ((rc = upload(&g_tables_v4[kind][dev], host_tab4)) ||
         (rc = upload(&g_tables[kind][dev], host_tab)) ||

@@ -966,6 +966,7 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
     uint32_t *__restrict__ out_lens, uint32_t n, FuseCrc fuse) {
   constexpr uint32_t kHdr = 61;  // RD_KAFKAP_MSGSET_V2_SIZE (rdkafka_proto.h:540)
   __shared__ uint32_t t0_mem[FIN ? 256 : 1];
+  __shared__ uint32_t s_w[64];
   __shared__ uint32_t s_sz[FIN ? 64 : 1];
   __shared__ uint32_t s_term[FIN ? 65 : 1];
   const int t = threadIdx.x;
@@ -985,25 +986,37 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
       stb(ob + 4, 0x60); stb(ob + 5, 0x40); stb(ob + 6, 0x82);
     }
     uint64_t pos = 7;
-    for (uint32_t k = 0; k < nb; ++k) {
-      const uintptr_t slot = ob + 7u + uint64_t(k) * kSlot;
-      // (the same word in every thread: saying so keeps the addresses below in scalar registers)
-      const uint32_t w = uint32_t(__builtin_amdgcn_readfirstlane(
-          int(ldb(slot) | (ldb(slot + 1) << 8) | (ldb(slot + 2) << 16) | (ldb(slot + 3) << 24))));
-      __syncthreads();  // everyone has read the size word before it may be overwritten
-      const bool raw = w & 0x80000000u;
-      const uint32_t sz = w & 0x7FFFFFFFu;
-      const uintptr_t from = raw ? ib + uint64_t(k) * kLz4Block : slot + 4u;
-      const uintptr_t to = ob + pos + 4u;
-      if (from != to) asm_slide<kAsmThreads>(to, from, sz, t);
-      if (t == 0) {
-        stb(ob + pos, w & 0xFFu); stb(ob + pos + 1, (w >> 8) & 0xFFu);
-        stb(ob + pos + 2, (w >> 16) & 0xFFu); stb(ob + pos + 3, w >> 24);
-        if (FIN && k < 64u) s_sz[k] = sz;
+    for (uint32_t k0 = 0; k0 < nb; k0 += 64u) {
+      // the size words of the next 64 slots, one per thread, before any of those blocks
+      // moves (a block's new place ends below the next slot, so it overwrites no size word
+      // that is still to be read -- and none of a later group)
+      const uint32_t kn = nb - k0 < 64u ? nb - k0 : 64u;
+      __syncthreads();
+      if (uint32_t(t) < kn) {
+        const uintptr_t slot = ob + 7u + uint64_t(k0 + uint32_t(t)) * kSlot;
+        s_w[t] = ldb(slot) | (ldb(slot + 1) << 8) | (ldb(slot + 2) << 16) | (ldb(slot + 3) << 24);
       }
       __syncthreads();
-      pos += 4u + sz;
+      for (uint32_t k = k0; k < k0 + kn; ++k) {
+        const uintptr_t slot = ob + 7u + uint64_t(k) * kSlot;
+        // (the same word in every thread: saying so keeps the addresses below in scalar registers)
+        const uint32_t w = uint32_t(__builtin_amdgcn_readfirstlane(int(s_w[k - k0])));
+        const bool raw = w & 0x80000000u;
+        const uint32_t sz = w & 0x7FFFFFFFu;
+        const uintptr_t from = raw ? ib + uint64_t(k) * kLz4Block : slot + 4u;
+        const uintptr_t to = ob + pos + 4u;
+        // (no barrier between blocks: block k + 1 is read from its own slot, which block k's
+        // new place does not reach, and written behind the barrier of its own move)
+        if (from != to) asm_slide<kAsmThreads>(to, from, sz, t);
+        if (t == 0) {
+          stb(ob + pos, w & 0xFFu); stb(ob + pos + 1, (w >> 8) & 0xFFu);
+          stb(ob + pos + 2, (w >> 16) & 0xFFu); stb(ob + pos + 3, w >> 24);
+          if (FIN && k < 64u) s_sz[k] = sz;
+        }
+        pos += 4u + sz;
+      }
     }
+    __syncthreads();
     const uint32_t flen = uint32_t(pos + 4u);
     if (t == 0) {
       stb(ob + pos, 0); stb(ob + pos + 1, 0); stb(ob + pos + 2, 0); stb(ob + pos + 3, 0);
@@ -1040,7 +1053,7 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
         if (uint32_t(t) < nb) {
           uint32_t after = 4u;                            // the end mark
           for (uint32_t j = uint32_t(t) + 1u; j < nb; ++j) after += 4u + s_sz[j];
-          s_term[t] = crcw_shift(fuse.block_crc[size_t(f) * 64u + uint32_t(t)], after, fuse.x2n);
+          s_term[t] = crcw_shift_lut(fuse.block_crc[size_t(f) * 64u + uint32_t(t)], after, fuse.x2n);
         } else if (t >= 64 && t < 128) {
           // the second wavefront: header bytes [21, 68) one per lane in a register, then the
           // byte-table chain over them (no memory access inside the chain)
@@ -1050,7 +1063,7 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
 #pragma unroll
           for (int j = 0; j < int(kHdr + 7u - 21u); ++j)
             r = t0[(r ^ uint32_t(__builtin_amdgcn_readlane(int(hb), j))) & 0xFFu] ^ (r >> 8);
-          if (t == 64) s_term[64] = crcw_shift(r, flen - 7u, fuse.x2n);
+          if (t == 64) s_term[64] = crcw_shift_lut(r, flen - 7u, fuse.x2n);
         }
         __syncthreads();
         uint32_t r = s_term[64];

@@ -73,7 +73,7 @@ __device__ __forceinline__ uint32_t wave_block_register(uint32_t w, uintptr_t sl
   uint32_t r = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) r = t4[(r ^ (w >> (8 * j))) & 0xFFu] ^ (r >> 8);
-  return crcw_shift(r, sz, fuse.x2n) ^ wave_crc_range(src, sz, false, t4, fuse.x2n, lane);
+  return crcw_shift_lut(r, sz, fuse.x2n) ^ wave_crc_range(src, sz, false, t4, fuse.x2n, lane);
 }
 
 // Behind block k of frame f (size word w stored at `slot`, the wave's stores retired by the

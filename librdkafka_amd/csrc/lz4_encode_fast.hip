@@ -285,7 +285,7 @@ __device__ __forceinline__ Meas round_measure(const BlockCtx &b, const Win &x, c
   }
   uint32_t fd = cz[kFastPairs - 1];
 #pragma unroll
-  for (int k = kFastPairs - 2; k >= 0; --k) fd = cz[k] + (cz[k] >> 6) * fd;
+  for (int k = kFastPairs - 2; k >= 0; --k) fd = cz[k] + __umul24(cz[k] >> 6, fd);  // (a full-rate multiply)
   fd >>= 3;
   m.len = 4 + int(fd < uint32_t(kFastLen - 4) ? fd : uint32_t(kFastLen - 4));
   if (m.len > b.mlim - i) m.len = b.mlim - i;
@@ -365,6 +365,7 @@ __device__ __forceinline__ void round_walk(BlockCtx &b, const Win &x, const Cand
   const uint32_t mc = uint32_t(len + bk) - 4u;
   const uint32_t off = uint32_t(i - y.c);
   const uint32_t lstart = uint32_t(R + prev);  // absolute literal start
+  b.qn = __builtin_amdgcn_readfirstlane(b.qn);  // (wave-uniform: keeps the count in a scalar register)
   if (b.qn + cnt > 64) flush_sequences(b, queue, lane);
   const int rank = int(__builtin_amdgcn_mbcnt_hi(uint32_t(chosen >> 32),
                                                  __builtin_amdgcn_mbcnt_lo(uint32_t(chosen), 0u)));

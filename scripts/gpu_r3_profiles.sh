@@ -27,7 +27,7 @@ run() {
     lz4hc12) $P lz4hc_compress_level12_1MiB_json "lz4hc_build_kernel,lz4hc_count_items_kernel,lz4hc_compress_blocks_kernel,lz4f_assemble_kernel" --workload lz4hc --level 12 --partitions 256 --steps 10 ;;
     snappyc) $P snappy_compress_1MiB_json "snappy_compress_fragments_kernel,snappy_assemble_kernel" --workload snappyc --partitions 256 --steps 10 ;;
     snappyd) $P snappy_uncompress_1MiB_json "snappy_scan_kernel,snappy_uncompress_kernel" --workload snappyd --partitions 1024 --steps 10 ;;
-    serialize) $P v2_record_serialize_1MiB_json "v2_batch_kernel,v2_chunk_kernel,v2_fixup_kernel,v2_write_kernel" --workload serialize --partitions 256 --steps 10 ;;
+    serialize) $P v2_record_serialize_1MiB_json "v2_batch_kernel,v2_chunk_kernel,v2_fixup_kernel,v2_write_kernel,crc32c_msgset_v2_split_kernel,crc32c_msgset_v2_combine_kernel" --workload serialize --partitions 256 --steps 10 ;;
     index) $P v2_record_index_1MiB_json "v2_index_spec_kernel,v2_index_kernel" --workload index --partitions 256 --steps 10 ;;
     legacy) $P v1_msgset_crc32_verify_1MiB_json "v01_crc_kernel" --workload legacy --partitions 256 --steps 10 ;;
     perf_tool) $P perf_tool_1M_x_100B_messages "v2_batch_kernel,v2_chunk_kernel,v2_fixup_kernel,v2_write_kernel,lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload perf_tool --steps 10 ;;

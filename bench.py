@@ -627,24 +627,46 @@ def bench_chain(args, rank, world, n=None, per_batch=9500):
     s = L._stream(None)
     lib = L.lib()
 
-    def write_step():
+    def write_step(mode=L.PRODUCER_EXACT):
         lib.rdk_hip_msgset_v2_sizes(C.byref(m), b.ctypes.data, n, L._ptr(rec_pos), L._ptr(sizes),
                                     L._ptr(max_ts), s)
         lib.rdk_hip_msgset_v2_write(C.byref(m), b.ctypes.data, n, L._ptr(rec_pos), L._ptr(sizes),
                                     L._ptr(max_ts), L._ptr(offs), L._ptr(sets), None, s)
         L.msgset_v2_finalize(sets, rec_offs, rec_lens, out, out_offs, out_caps, flens, blens, crcs,
-                             mode=L.PRODUCER_EXACT)
+                             mode=mode)
+
+    total = int(rl.sum())
+    # the same chain with the throughput compressor (reported beside the leg, which is the
+    # byte-identical one); its batches are CRC-verified and decoded back before the exact
+    # run overwrites them
+    fms, fkms = _timed(lambda: write_step(L.PRODUCER_FAST), args.steps, args.warmup, world)
+    if not bool((blens == flens + 61).all()):
+        raise SystemExit(f"rank {rank}: a JSON batch was left uncompressed (throughput compressor)")
+    fclen = int(flens.to(torch.int64).sum())
+    fdec = torch.empty(n * ((int(rl.max()) + 255) // 256 * 256) + 256, dtype=torch.uint8, device="cuda")
+    fdo = torch.arange(n, dtype=torch.int64, device="cuda") * ((int(rl.max()) + 255) // 256 * 256)
+    fdc = torch.full((n,), (int(rl.max()) + 255) // 256 * 256, dtype=torch.int32, device="cuda")
+    fdl, fst, fvst = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    L.msgset_v2_crc(out, out_offs, out_caps, fvst, L.V2_CRC_VERIFY)
+    L.lz4f_decompress_batch(out, out_offs + 61, flens, fdec, fdo, fdc, fdl, fst)
+    if int(fvst.abs().sum()) or int(fst.abs().sum()) or not bool((fdl == rec_lens).all()):
+        raise SystemExit(f"rank {rank}: the throughput compressor's batches do not verify / decode")
+    i0 = int(rec_offs[0])
+    if not torch.equal(fdec[:int(rl[0])], sets[i0:i0 + int(rl[0])]):
+        raise SystemExit(f"rank {rank}: the throughput compressor's first batch decodes to other records")
+    del fdec
+    fast = {"GB_per_s": round(total * world / (max_over_ranks(fms, world) / 1e3) / 1e9, 2),
+            "ms_per_step": round(fms, 4), "kernel_ms": round(fkms, 4), "ratio": round(total / fclen, 3)}
 
     wms, wkms = _timed(write_step, args.steps, args.warmup, world)
     if not bool((blens == flens + 61).all()):
         raise SystemExit(f"rank {rank}: a JSON batch was left uncompressed")
-    total = int(rl.sum())
     clen = int(flens.to(torch.int64).sum())
     writer = {"ms": wms, "kernel_ms": wkms, "bytes": total, "records": n,
               # messages read (metadata + payload), MessageSets written, then read by the
               # compressor, frames written, headers read + written
               "alg_bytes": payload + 48 * n * per_batch + 2 * (total + 61 * n) + clen + 2 * 61 * n,
-              "ratio": total / clen}
+              "ratio": total / clen, "fast": fast}
     # ---- reader over the finished batches
     dslot = (int(rl.max()) + 255) // 256 * 256
     dec = torch.empty(n * dslot + 256, dtype=torch.uint8, device="cuda")
@@ -1573,6 +1595,7 @@ def main():
             wr, rd = bench_chain(sub, rank, world, n=256)
             legs["writer_messages_to_batches_1MiB_json"] = leg_line(
                 "writer_messages_to_batches_1MiB_json", wr, LEG_STEPS, 1)
+            legs["writer_messages_to_batches_1MiB_json"]["with_throughput_compressor"] = wr["fast"]
             legs["reader_batches_to_rows_1MiB_json"] = leg_line(
                 "reader_batches_to_rows_1MiB_json", rd, LEG_STEPS, 1)
             prod = {}

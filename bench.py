@@ -756,22 +756,35 @@ def bench_perf_tool(args, rank, world, msgs=1000000):
     s = L._stream(None)
     lib = L.lib()
 
-    def step():
+    def step(mode=L.PRODUCER_EXACT):
         lib.rdk_hip_msgset_v2_sizes(C.byref(mm), b.ctypes.data, n, L._ptr(rec_pos), L._ptr(sizes),
                                     L._ptr(max_ts), s)
         lib.rdk_hip_msgset_v2_write(C.byref(mm), b.ctypes.data, n, L._ptr(rec_pos), L._ptr(sizes),
                                     L._ptr(max_ts), L._ptr(offs), L._ptr(sets), None, s)
         L.msgset_v2_finalize(sets, rec_offs, rec_lens, out, out_offs, out_caps, flens, blens, crcs,
-                             mode=L.PRODUCER_EXACT)
+                             mode=mode)
 
-    ms, kms = _timed(step, args.steps, args.warmup, world)
-    # gate: the reader side hands every message back
     st, dl, ds, cnt = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(4))
-    L.msgset_v2_crc(out, out_offs, out_caps, st, L.V2_CRC_VERIFY)
     dslot = (int(rl.max()) + 255) // 256 * 256
     dec = torch.empty(n * dslot + 256, dtype=torch.uint8, device="cuda")
     doffs = torch.arange(n, dtype=torch.int64, device="cuda") * dslot
     dcaps = torch.full((n,), dslot, dtype=torch.int32, device="cuda")
+    # the same steps with the throughput compressor, reported beside the leg (which is the
+    # byte-identical one): its batches are verified and decoded back to the records
+    fms, fkms = _timed(lambda: step(L.PRODUCER_FAST), args.steps, args.warmup, world)
+    L.msgset_v2_crc(out, out_offs, out_caps, st, L.V2_CRC_VERIFY)
+    L.lz4f_decompress_batch(out, out_offs + 61, flens, dec, doffs, dcaps, dl, ds)
+    i0, l0 = int(rec_offs[0]), int(rl[0])
+    if int(st.abs().sum()) or int(ds.abs().sum()) or not bool((dl == rec_lens).all()) or \
+            not bool((blens == flens + 61).all()) or not torch.equal(dec[:l0], sets[i0:i0 + l0]):
+        raise SystemExit(f"rank {rank}: the throughput compressor's perf-tool batches do not verify / decode")
+    fast = {"msgs_per_s": round(msgs * world / (max_over_ranks(fms, world) / 1e3), 1),
+            "ms_per_step": round(fms, 4), "kernel_ms": round(fkms, 4),
+            "ratio": round(int(rl.sum()) / int(flens.to(torch.int64).sum()), 3)}
+
+    ms, kms = _timed(step, args.steps, args.warmup, world)
+    # gate: the reader side hands every message back
+    L.msgset_v2_crc(out, out_offs, out_caps, st, L.V2_CRC_VERIFY)
     L.lz4f_decompress_batch(out, out_offs + 61, flens, dec, doffs, dcaps, dl, ds)
     row_offs = torch.tensor(np.asarray([f for f, _ in spec], np.int64), device="cuda")
     row_caps = torch.tensor(np.asarray([c for _, c in spec], np.int32), device="cuda")
@@ -787,7 +800,7 @@ def bench_perf_tool(args, rank, world, msgs=1000000):
     clen = int(flens.to(torch.int64).sum())
     return {"ms": ms, "kernel_ms": kms, "bytes": total, "records": n, "messages": msgs,
             "alg_bytes": 100 + 48 * msgs + 2 * (total + 61 * n) + clen + 2 * 61 * n,
-            "ratio": total / clen, "host_sample": (m, spec)}
+            "ratio": total / clen, "host_sample": (m, spec), "fast": fast}
 
 
 def cpu_baseline_perf_tool(m, spec, seconds=6.0):
@@ -1537,6 +1550,7 @@ def main():
             pres.pop("host_sample", None)
             pl = leg_line("perf_tool_1M_x_100B_messages", pres, LEG_STEPS, 1, pcpu)
             pl["msgs_per_s"] = round(pres["messages"] / (pres["ms"] / 1e3), 1)
+            pl["with_throughput_compressor"] = pres["fast"]
             legs["perf_tool_1M_x_100B_messages"] = pl
             del pres
             torch.cuda.empty_cache()

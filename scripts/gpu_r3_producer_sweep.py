@@ -8,7 +8,8 @@ import librdkafka_amd as L
 import bench
 L.init(0)
 n = 2048
-for ns, th, slot in ((8, 1, 128), (8, 2, 128), (2, 4, 64), (4, 4, 32), (2, 8, 32), (4, 8, 16)):
+for ns, th, slot in ((8, 1, 128), (4, 1, 64), (8, 2, 128), (4, 2, 64), (2, 4, 64), (3, 4, 64), (4, 4, 32),
+                     (2, 4, 128), (2, 8, 32), (3, 8, 32), (2, 8, 64), (4, 8, 16)):
     os.environ["RDK_BENCH_PRODUCER_NSLOTS"] = str(ns)
     r = bench.bench_producer(argparse.Namespace(steps=2, warmup=1, partitions=n), 0, 1, n=n, threads=th,
                              slot_mib=slot)

@@ -894,63 +894,6 @@ __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
   }
 }
 
-// The assembler's block move: sz bytes from `from` down to `to` (to < from in the same buffer,
-// or another buffer), by the whole workgroup.  The destination is cut at its 16-byte
-// boundaries: up to 15 head bytes, whole 16-byte units, up to 15 tail bytes.  A unit is
-// fetched as five dwords around its source (the source is not aligned to the destination; the
-// fetch goes through a range-checked resource, so it never reads past the block) and stored
-// as one aligned 16-byte word.  Each step reads four units per thread, then -- behind a
-// barrier, because a step's destination may overlap its own source -- writes them; the head
-// travels with the first step and the tail with the last, whose sources nothing before them
-// overwrites (a step's destination ends below the next step's source).
-template <uint32_t kAsmThreads>
-__device__ __forceinline__ void asm_slide(uintptr_t to, uintptr_t from, uint32_t sz, int t) {
-  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(1))) u4 g_u4;
-  const uint32_t head0 = uint32_t(-intptr_t(to)) & 15u;
-  const uint32_t head = head0 < sz ? head0 : sz;
-  const uint32_t units = (sz - head) >> 4;
-  const uint32_t tail = sz - head - (units << 4);
-  const uint32_t fa = uint32_t(from & 3u);
-  const rsrc_t rs = block_rsrc(from - fa, (from + sz + 3u) & ~uintptr_t(3));
-  const uint32_t sh = (fa + head) & 3u;  // a unit's first byte inside its first dword
-  constexpr uint32_t kPer = 4;
-  for (uint32_t u0 = 0;; u0 += kAsmThreads * kPer) {
-    const bool first = u0 == 0u, last = u0 + kAsmThreads * kPer >= units;
-    u4 a[kPer];
-    uint32_t e[kPer];
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j) {
-      const uint32_t u = u0 + uint32_t(t) + kAsmThreads * j;
-      const uint32_t off = u < units ? ((fa + head + (u << 4)) & ~3u) : kNoLoad;
-      a[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-      e[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 16u, 0, 0);
-    }
-    // head and tail bytes, one per thread (threads 0..14 and 16..30)
-    uint32_t hb = 0, tb = 0;
-    const bool do_h = first && uint32_t(t) < head;
-    const bool do_t = last && uint32_t(t) >= 16u && uint32_t(t) - 16u < tail;
-    if (do_h) hb = ldb(from + uint32_t(t));
-    if (do_t) tb = ldb(from + head + (units << 4) + (uint32_t(t) - 16u));
-    __syncthreads();  // the step is fully read before any of it is written
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j) {
-      const uint32_t u = u0 + uint32_t(t) + kAsmThreads * j;
-      if (u < units) {
-        u4 v;
-        v.x = __builtin_amdgcn_alignbyte(a[j].y, a[j].x, sh);
-        v.y = __builtin_amdgcn_alignbyte(a[j].z, a[j].y, sh);
-        v.z = __builtin_amdgcn_alignbyte(a[j].w, a[j].z, sh);
-        v.w = __builtin_amdgcn_alignbyte(e[j], a[j].w, sh);
-        *(g_u4 *)(to + head + (u << 4)) = v;
-      }
-    }
-    if (do_h) stb(to + uint32_t(t), hb);
-    if (do_t) stb(to + head + (units << 4) + (uint32_t(t) - 16u), tb);
-    if (last) break;
-  }
-}
-
 // One workgroup per frame: header (lz4frame.c:671-701), size words, blocks
 // slid down from their slots (raw blocks copied from the input), end mark.
 // FIN: the frame sits 61 bytes into a MsgVersion 2 batch slot and the workgroup also
@@ -965,13 +908,13 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
     const uint32_t *__restrict__ in_lens, uint8_t *out, const uint64_t *__restrict__ out_offs,
     uint32_t *__restrict__ out_lens, uint32_t n, FuseCrc fuse) {
   constexpr uint32_t kHdr = 61;  // RD_KAFKAP_MSGSET_V2_SIZE (rdkafka_proto.h:540)
-  __shared__ uint32_t t0_mem[FIN ? 256 : 1];
+  __shared__ uint32_t t0_mem[FIN ? 1024 : 1];  // the four byte tables; the first is T0
   __shared__ uint32_t s_w[64];
   __shared__ uint32_t s_sz[FIN ? 64 : 1];
   __shared__ uint32_t s_term[FIN ? 65 : 1];
   const int t = threadIdx.x;
   if (FIN) {
-    if (t < 256) t0_mem[t] = fuse.t0[t];
+    for (uint32_t i = uint32_t(t); i < 1024u; i += kAsmThreads) t0_mem[i] = fuse.t0[i];
     __syncthreads();
   }
   crcw_lds_u32 *t0 = (crcw_lds_u32 *)t0_mem;
@@ -1030,8 +973,7 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
       const bool compressed = flen <= len;
       const uint32_t payload = compressed ? flen : len;
       __syncthreads();                                    // the frame is complete
-      if (!compressed)                                    // keep the records plain
-        for (uint32_t k = t; k < len; k += kAsmThreads) stb(ob + k, ldb(ib + k));
+      if (!compressed) asm_slide<kAsmThreads>(ob, ib, len, t);  // keep the records plain
       if (uint32_t(t) < kHdr) {
         uint32_t v = ldb(hdr + uint32_t(t));
         const uint32_t length = kHdr + payload - 12u;
@@ -1070,13 +1012,20 @@ __global__ __launch_bounds__(kAsmThreads) void lz4f_assemble_kernel(
         for (uint32_t k = 0; k < nb; ++k) r ^= s_term[k];
         crc = ~r;
       } else {
-        // plain records, or more blocks than registers were kept for: the first wavefront
-        // runs over the finished bytes
-        crc = 0;
-        if (t < 64) {
-          const uint32_t total = kHdr - 21u + payload;
-          crc = ~(crcw_shift(~0u, total, fuse.x2n) ^ wave_crc_raw(bo + 21u, total, t0, fuse.x2n, t));
-        }
+        // plain records, or more blocks than registers were kept for: the workgroup's waves
+        // run over the finished bytes, a slice each, and the slices combine by shifting
+        constexpr uint32_t kWaves = kAsmThreads / 64u;
+        const uint32_t total = kHdr - 21u + payload;
+        const uint32_t wv = uint32_t(t) >> 6, ln = uint32_t(t) & 63u;
+        const uint32_t per = ((total + kWaves - 1u) / kWaves + 15u) & ~15u;
+        const uint32_t s0 = wv * per;
+        const uint32_t sl = s0 >= total ? 0u : (total - s0 < per ? total - s0 : per);
+        const uint32_t r = wave_crc_range(bo + 21u + s0, sl, wv == 0u, t0, fuse.x2n, int(ln));
+        if (ln == 0u) s_term[wv] = sl || wv == 0u ? crcw_shift_lut(r, total - s0 - sl, fuse.x2n) : 0u;
+        __syncthreads();
+        uint32_t x = 0;
+        for (uint32_t k = 0; k < kWaves; ++k) x ^= s_term[k];
+        crc = ~x;
       }
       if (t == 0) {
         stb(bo + 17, crc >> 24); stb(bo + 18, (crc >> 16) & 0xFFu);

@@ -75,6 +75,11 @@ __device__ __forceinline__ uint32_t hash4(uint32_t seq) {  // LZ4_hash4, lz4.c:6
 }
 
 constexpr uint32_t kShortLit = 16;  // literal runs copied by their own lane
+#ifndef RDK_FAST_SPARSE
+#define RDK_FAST_SPARSE 1  // 0: data that stops matching stays at one probe per position (A/B runs)
+#endif
+constexpr int kSparse = 8;      // stride of the rounds over data that has stopped matching
+constexpr int kColdRounds = 16;  // dense rounds without a verified match before they start (1 KiB)
 
 struct BlockCtx {
   uintptr_t src, dst;
@@ -88,6 +93,9 @@ struct BlockCtx {
   int rend;            // positions at or past it belong to the next phase: not entered yet
   int nseq, mbytes;    // sequences so far; match bytes so far, a partial sum per lane (the stride decision)
   bool full;           // the block does not fit in olimit bytes: nothing more is written
+  int cold;            // rounds in a row without a single verified match (dense rounds)
+  bool sparse;         // the rounds in progress are the sparse ones
+  bool trig;           // this run of rounds was told to end (rend pulled in): the mode changes
 };
 
 // Per round the lane's own 36-byte window (Win, loaded three rounds ahead),
@@ -342,7 +350,31 @@ __device__ __forceinline__ void round_walk(BlockCtx &b, const Win &x, const Cand
     const int f2 = (S * q + L + S - 1) / S;
     q = __builtin_amdgcn_readfirstlane(encode(f2 < 64 ? vm >> f2 : 0ull, f2));
   }
-  if (!chosen) return;
+  // Data without matches (already compressed, encrypted) is not worth 64 probes per 64
+  // positions: after kColdRounds rounds in a row without one verified match the block goes
+  // on at every kSparse-th position -- what the reference's growing search step does
+  // (lz4.c:886).  The change takes effect by pulling the end of this run of rounds in to the
+  // end of the NEXT round, whose positions the lookup ahead has already entered: the loop
+  // then drains by itself.  (Only the position-by-position rounds count: a block that has
+  // earned the stride of two matches well, and its rounds keep their loop bound in a
+  // register.)  The first match a sparse round finds ends the sparse rounds at once: only
+  // that match is taken, and the dense rounds resume right behind it (fast_block).
+  if constexpr (S == kSparse) chosen &= 0ull - chosen;
+  if (!chosen) {
+    if constexpr (S == 1 && RDK_FAST_SPARSE) {
+      if (!vm && xin < 64 * S && ++b.cold == kColdRounds) {
+        b.rend = min(b.rend, R + 2 * 64 * S);
+        b.trig = true;
+      }
+    }
+    return;
+  }
+  if constexpr (S == kSparse) {
+    b.rend = min(b.rend, R + 64 * S);
+    b.trig = true;
+  } else if constexpr (S == 1) {
+    b.cold = 0;
+  }
   const int lastq = 63 - int(__builtin_clzll(chosen));
   b.p = R + S * lastq + __builtin_amdgcn_readlane(len, lastq);
 
@@ -401,21 +433,27 @@ __device__ __forceinline__ void round_step(BlockCtx &b, const Win &cur, Win &nex
 template <int S>
 __device__ __forceinline__ void fast_rounds(BlockCtx &b, FastLds *lds, int r0, int lane) {
   constexpr int kSpan = 64 * S;
-  const int last = min(b.mfl, b.rend - 1);  // the last position that starts a round's work
-  if (r0 > last) return;
+  // the last position that starts a round's work (b.rend may be pulled in by a round, see
+  // round_walk; wave-uniform, and said to be, so that the loop's control stays scalar)
+  const int last_fixed = min(b.mfl, b.rend - 1);
+  const auto last_pos = [&] {
+    if constexpr (S == 2) return last_fixed;
+    else return min(b.mfl, __builtin_amdgcn_readfirstlane(b.rend) - 1);
+  };
+  if (r0 > last_pos()) return;
   Win W0, W1, W2, W3;
   Cand C0, C1;
   round_load<S>(b, W0, r0, lane);
   round_load<S>(b, W1, r0 + kSpan, lane);
   round_load<S>(b, W2, r0 + 2 * kSpan, lane);
   round_gather<S>(b, C0, round_lookup<S>(b, W0, r0, (lds_u16 *)lds->table, lane), r0, lane);
-  for (int R = r0; R <= last; R += 4 * kSpan) {
+  for (int R = r0; R <= last_pos(); R += 4 * kSpan) {
     round_step<S>(b, W0, W1, W3, C0, C1, R, lds, lane);
-    if (R + kSpan > last) break;
+    if (R + kSpan > last_pos()) break;
     round_step<S>(b, W1, W2, W0, C1, C0, R + kSpan, lds, lane);
-    if (R + 2 * kSpan > last) break;
+    if (R + 2 * kSpan > last_pos()) break;
     round_step<S>(b, W2, W3, W1, C0, C1, R + 2 * kSpan, lds, lane);
-    if (R + 3 * kSpan > last) break;
+    if (R + 3 * kSpan > last_pos()) break;
     round_step<S>(b, W3, W0, W2, C1, C0, R + 3 * kSpan, lds, lane);
   }
 }
@@ -454,19 +492,33 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, FastLds *lds, int
   b.nseq = b.mbytes = 0;
   b.full = false;
 
-  b.rend = RDK_FAST_STRIDE2 ? kProbe : n;
-  for (int r0 = 0;;) {  // (a loop so that the one-by-one rounds exist once in the code)
-    fast_rounds<1>(b, lds, r0, lane);
-    if (__builtin_amdgcn_readfirstlane(int(b.full)) || b.rend >= n || b.mfl < b.rend) break;
-    r0 = b.rend;
-    b.rend = n;
-    const int nseq = __builtin_amdgcn_readfirstlane(b.nseq);
-    uint32_t mbytes;
-    wave_excl_scan(uint32_t(b.mbytes), mbytes);
-    if (nseq > 0 && int(mbytes) >= kStride2MinMatch * nseq) {
-      fast_rounds<2>(b, lds, r0, lane);
-      break;
+  b.sparse = b.trig = false;
+  int S = 1;                        // stride of the dense rounds
+  bool decided = !RDK_FAST_STRIDE2;  // ... once the block's first kProbe positions have decided it
+  for (int r0 = 0;;) {
+    if (!decided && r0 >= kProbe) {
+      decided = true;
+      const int nseq = __builtin_amdgcn_readfirstlane(b.nseq);
+      uint32_t mbytes;
+      wave_excl_scan(uint32_t(b.mbytes), mbytes);
+      if (nseq > 0 && int(mbytes) >= kStride2MinMatch * nseq) S = 2;
     }
+    b.rend = (!decided && !b.sparse) ? kProbe : n;
+    b.cold = 0;
+    if (b.sparse) fast_rounds<kSparse>(b, lds, r0, lane);
+    else if (S == 2) fast_rounds<2>(b, lds, r0, lane);
+    else fast_rounds<1>(b, lds, r0, lane);
+    const int rend = __builtin_amdgcn_readfirstlane(b.rend);
+    if (__builtin_amdgcn_readfirstlane(int(b.full)) || rend >= n || b.mfl < rend) break;
+    r0 = rend;
+    if (__builtin_amdgcn_readfirstlane(int(b.trig))) {
+      // (out of the sparse rounds: on from the end of the match that ended them; the few
+      // positions the last lookup ahead entered for a round that was not parsed find
+      // themselves in the table and go without a candidate)
+      if (b.sparse) r0 = __builtin_amdgcn_readfirstlane(b.p);
+      b.sparse = !b.sparse;
+    }
+    b.trig = false;
   }
   flush_sequences(b, (lds_u2 *)lds->queue, lane);
   if (b.full) return 0;

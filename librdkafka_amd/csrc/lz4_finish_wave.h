@@ -42,7 +42,7 @@ __device__ __forceinline__ void wave_finish_single(uintptr_t ob, uintptr_t ib, u
     if (lane < 7) stb(ob + uint32_t(lane), uint32_t(0x00824060184D2204ull >> (8 * lane)) & 0xFFu);
     if (lane >= 8 && lane < 12) stb(ob + 11u + sz + uint32_t(lane - 8), 0u);
   } else {
-    wave_copy_bytes(ob, ib, len, lane);  // keep the records plain
+    asm_slide<64, false>(ob, ib, len, lane);  // keep the records plain
   }
   if (uint32_t(lane) < kFinHdr) {
     uint32_t v = ldb(hdr + uint32_t(lane));

@@ -104,6 +104,64 @@ __device__ __forceinline__ void wave_copy_bytes(uintptr_t d, uintptr_t s, uint32
   }
 }
 
+// A block move by kThreads threads: sz bytes from `from` down to `to` (to < from in the same
+// buffer, or another buffer).  The destination is cut at its 16-byte
+// boundaries: up to 15 head bytes, whole 16-byte units, up to 15 tail bytes.  A unit is
+// fetched as five dwords around its source (the source is not aligned to the destination; the
+// fetch goes through a range-checked resource, so it never reads past the block) and stored
+// as one aligned 16-byte word.  Each step reads four units per thread, then -- behind a
+// barrier, because a step's destination may overlap its own source -- writes them; the head
+// travels with the first step and the tail with the last, whose sources nothing before them
+// overwrites (a step's destination ends below the next step's source).
+// kBarrier = false: one wavefront moving between buffers that do not overlap.
+template <uint32_t kAsmThreads, bool kBarrier = true>
+__device__ __forceinline__ void asm_slide(uintptr_t to, uintptr_t from, uint32_t sz, int t) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1))) u4 g_u4;
+  const uint32_t head0 = uint32_t(-intptr_t(to)) & 15u;
+  const uint32_t head = head0 < sz ? head0 : sz;
+  const uint32_t units = (sz - head) >> 4;
+  const uint32_t tail = sz - head - (units << 4);
+  const uint32_t fa = uint32_t(from & 3u);
+  const rsrc_t rs = block_rsrc(from - fa, (from + sz + 3u) & ~uintptr_t(3));
+  const uint32_t sh = (fa + head) & 3u;  // a unit's first byte inside its first dword
+  constexpr uint32_t kPer = 4;
+  for (uint32_t u0 = 0;; u0 += kAsmThreads * kPer) {
+    const bool first = u0 == 0u, last = u0 + kAsmThreads * kPer >= units;
+    u4 a[kPer];
+    uint32_t e[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      const uint32_t u = u0 + uint32_t(t) + kAsmThreads * j;
+      const uint32_t off = u < units ? ((fa + head + (u << 4)) & ~3u) : kNoLoad;
+      a[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      e[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 16u, 0, 0);
+    }
+    // head and tail bytes, one per thread (threads 0..14 and 16..30)
+    uint32_t hb = 0, tb = 0;
+    const bool do_h = first && uint32_t(t) < head;
+    const bool do_t = last && uint32_t(t) >= 16u && uint32_t(t) - 16u < tail;
+    if (do_h) hb = ldb(from + uint32_t(t));
+    if (do_t) tb = ldb(from + head + (units << 4) + (uint32_t(t) - 16u));
+    if (kBarrier) __syncthreads();  // the step is fully read before any of it is written
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      const uint32_t u = u0 + uint32_t(t) + kAsmThreads * j;
+      if (u < units) {
+        u4 v;
+        v.x = __builtin_amdgcn_alignbyte(a[j].y, a[j].x, sh);
+        v.y = __builtin_amdgcn_alignbyte(a[j].z, a[j].y, sh);
+        v.z = __builtin_amdgcn_alignbyte(a[j].w, a[j].z, sh);
+        v.w = __builtin_amdgcn_alignbyte(e[j], a[j].w, sh);
+        *(g_u4 *)(to + head + (u << 4)) = v;
+      }
+    }
+    if (do_h) stb(to + uint32_t(t), hb);
+    if (do_t) stb(to + head + (units << 4) + (uint32_t(t) - 16u), tb);
+    if (last) break;
+  }
+}
+
 __device__ __forceinline__ uint32_t ext_bytes(uint32_t v) {  // 255-run encoding length
   return v >= 15u ? (v - 15u) / 255u + 1u : 0u;
 }

@@ -463,6 +463,32 @@ def test_fast_compress_ratio_within_5pct(engine, oracle_mod, units):
         assert r_gpu >= 0.95 * r_ref, (i, r_gpu, r_ref)
 
 
+def test_fast_compress_data_that_stops_and_starts_matching(engine, oracle_mod):
+    """Stretches without matches (random bytes) put the wave engine's rounds at every eighth
+    position, the first match brings them back: blocks that change between the two, at
+    several stretch lengths and in both orders, decode to their input, and the ratio stays
+    within 5 % of the reference's (whose own search step grows over such stretches)."""
+    rnd = random.Random(46)
+    inputs = []
+    for stretch in (600, 1100, 1400, 2048, 5000, 20000, 70000):
+        parts = []
+        for j in range(12):
+            parts.append(rnd.randbytes(stretch) if j % 2 == 0 else W.gen_json(stretch, 40 + j))
+        inputs.append(b"".join(parts))
+        inputs.append(b"".join(parts[1:]))
+    # sparse matches: a 24-byte string every few hundred random bytes
+    key = rnd.randbytes(24)
+    inputs.append(b"".join(rnd.randbytes(rnd.randrange(100, 700)) + key for _ in range(400)))
+    inputs.append(rnd.randbytes(300000))
+    frames = _fast_compress(engine, inputs)
+    for i, (b, fr) in enumerate(zip(inputs, frames)):
+        e, out = oracle_mod.rdk_lz4_decompress(fr)
+        assert e == 0 and out == b, (i, len(b), e)
+        assert engine.rd_kafka_lz4_decompress(1, 0, fr) == (0, b), i
+        ref = oracle_mod.rdk_lz4_compress(b)[1]
+        assert len(b) / len(fr) >= 0.95 * (len(b) / len(ref)), (i, len(b), len(fr), len(ref))
+
+
 def test_units_engine_equals_the_sequential_model(engine):
     """The workgroup-per-block engine's output is defined by tests/sim/lz4_units_sim.cpp (candidates
     in position order, units parsed on their own, stitched in order): the kernel's frames

@@ -20,7 +20,8 @@
 //     worked out for itself; only matches longer than 28 bytes go back to memory (64 bytes
 //     per wave step);
 //   * a block whose first 2 KiB match well is probed at every second position from there on
-//     (every position is still entered into the table);
+//     (every position is still entered into the table); data that has stopped matching
+//     altogether is probed at every eighth position until a match turns up;
 //   * sequences are queued in LDS and emitted 64 at a time: a wave prefix sum places every
 //     sequence, each lane writes its token, length bytes, literals and offset (LZ4 block
 //     format, lz4.c:961-1073).

@@ -591,7 +591,7 @@ def bench_index(args, rank, world, n=None, per_batch=9500):
             "host_sample": (base, per_batch)}
 
 
-def bench_chain(args, rank, world, n=None, per_batch=9500):
+def bench_chain(args, rank, world, n=None, per_batch=9500, with_fast=True):
     """Both directions whole, every stage on the device and chained on one stream as a
     broker thread would chain them, over ~1 MiB batches of ~100-byte JSON messages:
       writer: record sizes + record writer (rdkafka_msgset_writer.c:652-754, :1117-1207)
@@ -636,27 +636,29 @@ def bench_chain(args, rank, world, n=None, per_batch=9500):
                              mode=mode)
 
     total = int(rl.sum())
-    # the same chain with the throughput compressor (reported beside the leg, which is the
-    # byte-identical one); its batches are CRC-verified and decoded back before the exact
-    # run overwrites them
-    fms, fkms = _timed(lambda: write_step(L.PRODUCER_FAST), args.steps, args.warmup, world)
-    if not bool((blens == flens + 61).all()):
-        raise SystemExit(f"rank {rank}: a JSON batch was left uncompressed (throughput compressor)")
-    fclen = int(flens.to(torch.int64).sum())
-    fdec = torch.empty(n * ((int(rl.max()) + 255) // 256 * 256) + 256, dtype=torch.uint8, device="cuda")
-    fdo = torch.arange(n, dtype=torch.int64, device="cuda") * ((int(rl.max()) + 255) // 256 * 256)
-    fdc = torch.full((n,), (int(rl.max()) + 255) // 256 * 256, dtype=torch.int32, device="cuda")
-    fdl, fst, fvst = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
-    L.msgset_v2_crc(out, out_offs, out_caps, fvst, L.V2_CRC_VERIFY)
-    L.lz4f_decompress_batch(out, out_offs + 61, flens, fdec, fdo, fdc, fdl, fst)
-    if int(fvst.abs().sum()) or int(fst.abs().sum()) or not bool((fdl == rec_lens).all()):
-        raise SystemExit(f"rank {rank}: the throughput compressor's batches do not verify / decode")
-    i0 = int(rec_offs[0])
-    if not torch.equal(fdec[:int(rl[0])], sets[i0:i0 + int(rl[0])]):
-        raise SystemExit(f"rank {rank}: the throughput compressor's first batch decodes to other records")
-    del fdec
-    fast = {"GB_per_s": round(total * world / (max_over_ranks(fms, world) / 1e3) / 1e9, 2),
-            "ms_per_step": round(fms, 4), "kernel_ms": round(fkms, 4), "ratio": round(total / fclen, 3)}
+    fast = None
+    if with_fast:  # (not when the workload runs alone: a profile of the leg then holds its kernels only)
+        # the same chain with the throughput compressor (reported beside the leg, which is the
+        # byte-identical one); its batches are CRC-verified and decoded back before the exact
+        # run overwrites them
+        fms, fkms = _timed(lambda: write_step(L.PRODUCER_FAST), args.steps, args.warmup, world)
+        if not bool((blens == flens + 61).all()):
+            raise SystemExit(f"rank {rank}: a JSON batch was left uncompressed (throughput compressor)")
+        fclen = int(flens.to(torch.int64).sum())
+        fdec = torch.empty(n * ((int(rl.max()) + 255) // 256 * 256) + 256, dtype=torch.uint8, device="cuda")
+        fdo = torch.arange(n, dtype=torch.int64, device="cuda") * ((int(rl.max()) + 255) // 256 * 256)
+        fdc = torch.full((n,), (int(rl.max()) + 255) // 256 * 256, dtype=torch.int32, device="cuda")
+        fdl, fst, fvst = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+        L.msgset_v2_crc(out, out_offs, out_caps, fvst, L.V2_CRC_VERIFY)
+        L.lz4f_decompress_batch(out, out_offs + 61, flens, fdec, fdo, fdc, fdl, fst)
+        if int(fvst.abs().sum()) or int(fst.abs().sum()) or not bool((fdl == rec_lens).all()):
+            raise SystemExit(f"rank {rank}: the throughput compressor's batches do not verify / decode")
+        i0 = int(rec_offs[0])
+        if not torch.equal(fdec[:int(rl[0])], sets[i0:i0 + int(rl[0])]):
+            raise SystemExit(f"rank {rank}: the throughput compressor's first batch decodes to other records")
+        del fdec
+        fast = {"GB_per_s": round(total * world / (max_over_ranks(fms, world) / 1e3) / 1e9, 2),
+                "ms_per_step": round(fms, 4), "kernel_ms": round(fkms, 4), "ratio": round(total / fclen, 3)}
 
     wms, wkms = _timed(write_step, args.steps, args.warmup, world)
     if not bool((blens == flens + 61).all()):
@@ -722,7 +724,7 @@ def perf_tool_messages(msgs):
     return m, spec
 
 
-def bench_perf_tool(args, rank, world, msgs=1000000):
+def bench_perf_tool(args, rank, world, msgs=1000000, with_fast=True):
     """configs[0]'s workload through the engine, device-resident: 1M x 100-byte messages of
     the perf tool's payload -> record sizes + record writer (rdkafka_msgset_writer.c:652-754)
     -> rdk_hip_msgset_v2_finalize with frames byte-identical to rd_kafka_lz4_compress ->
@@ -769,18 +771,20 @@ def bench_perf_tool(args, rank, world, msgs=1000000):
     dec = torch.empty(n * dslot + 256, dtype=torch.uint8, device="cuda")
     doffs = torch.arange(n, dtype=torch.int64, device="cuda") * dslot
     dcaps = torch.full((n,), dslot, dtype=torch.int32, device="cuda")
-    # the same steps with the throughput compressor, reported beside the leg (which is the
-    # byte-identical one): its batches are verified and decoded back to the records
-    fms, fkms = _timed(lambda: step(L.PRODUCER_FAST), args.steps, args.warmup, world)
-    L.msgset_v2_crc(out, out_offs, out_caps, st, L.V2_CRC_VERIFY)
-    L.lz4f_decompress_batch(out, out_offs + 61, flens, dec, doffs, dcaps, dl, ds)
-    i0, l0 = int(rec_offs[0]), int(rl[0])
-    if int(st.abs().sum()) or int(ds.abs().sum()) or not bool((dl == rec_lens).all()) or \
-            not bool((blens == flens + 61).all()) or not torch.equal(dec[:l0], sets[i0:i0 + l0]):
-        raise SystemExit(f"rank {rank}: the throughput compressor's perf-tool batches do not verify / decode")
-    fast = {"msgs_per_s": round(msgs * world / (max_over_ranks(fms, world) / 1e3), 1),
-            "ms_per_step": round(fms, 4), "kernel_ms": round(fkms, 4),
-            "ratio": round(int(rl.sum()) / int(flens.to(torch.int64).sum()), 3)}
+    fast = None
+    if with_fast:  # (not when the workload runs alone: a profile of the leg then holds its kernels only)
+        # the same steps with the throughput compressor, reported beside the leg (which is the
+        # byte-identical one): its batches are verified and decoded back to the records
+        fms, fkms = _timed(lambda: step(L.PRODUCER_FAST), args.steps, args.warmup, world)
+        L.msgset_v2_crc(out, out_offs, out_caps, st, L.V2_CRC_VERIFY)
+        L.lz4f_decompress_batch(out, out_offs + 61, flens, dec, doffs, dcaps, dl, ds)
+        i0, l0 = int(rec_offs[0]), int(rl[0])
+        if int(st.abs().sum()) or int(ds.abs().sum()) or not bool((dl == rec_lens).all()) or \
+                not bool((blens == flens + 61).all()) or not torch.equal(dec[:l0], sets[i0:i0 + l0]):
+            raise SystemExit(f"rank {rank}: the throughput compressor's perf-tool batches do not verify / decode")
+        fast = {"msgs_per_s": round(msgs * world / (max_over_ranks(fms, world) / 1e3), 1),
+                "ms_per_step": round(fms, 4), "kernel_ms": round(fkms, 4),
+                "ratio": round(int(rl.sum()) / int(flens.to(torch.int64).sum()), 3)}
 
     ms, kms = _timed(step, args.steps, args.warmup, world)
     # gate: the reader side hands every message back
@@ -1422,9 +1426,9 @@ def main():
         elif args.workload == "legacy":
             res = bench_legacy(args, rank, world, n=args.partitions)
         elif args.workload == "perf_tool":
-            res = bench_perf_tool(args, rank, world)
+            res = bench_perf_tool(args, rank, world, with_fast=False)
         elif args.workload.startswith("chain"):
-            wr, rd = bench_chain(args, rank, world, n=args.partitions)
+            wr, rd = bench_chain(args, rank, world, n=args.partitions, with_fast=False)
             res = wr if args.workload == "chain_writer" else rd
         elif args.workload.startswith("snappy"):
             res = bench_snappy(args, rank, world, n=args.partitions,

@@ -840,6 +840,32 @@ __device__ int window_block(uintptr_t src, int n, uintptr_t dst, lds_u16 *table,
 // One wavefront per block.  Block k of frame f goes to the worst-case slot
 // at out_offs[f] + 7 + k*kSlot as [LE32 size word][payload]; a block stored
 // raw gets only its size word (payload is taken from the input later).
+// max over frames of ceil(len / 64 KiB), one workgroup
+__global__ __launch_bounds__(1024) void lz4f_max_blocks_kernel(const uint32_t *__restrict__ in_lens,
+                                                              uint32_t n, uint32_t *__restrict__ out) {
+  __shared__ uint32_t part[16];
+  uint32_t m = 0;
+  for (uint32_t f = threadIdx.x; f < n; f += 1024u) {
+    const uint32_t nb = (in_lens[f] + kLz4Block - 1) / kLz4Block;
+    m = nb > m ? nb : m;
+  }
+  for (int d = 32; d; d >>= 1) {
+    const uint32_t o = uint32_t(__shfl_xor(int(m), d));
+    m = o > m ? o : m;
+  }
+  if ((threadIdx.x & 63u) == 0u) part[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; ++w) m = part[w] > m ? part[w] : m;
+    *out = m;
+  }
+}
+
+void lz4f_max_blocks_launch(const uint32_t *d_in_lens, uint32_t n, uint32_t *d_max_nb, void *stream) {
+  hipLaunchKernelGGL(lz4f_max_blocks_kernel, dim3(1), dim3(1024), 0, static_cast<hipStream_t>(stream),
+                     d_in_lens, n, d_max_nb);
+}
+
 template <bool WINDOWS>
 __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_offs,
@@ -852,7 +878,14 @@ __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
   uint16_t *table_mem = reinterpret_cast<uint16_t *>(lds_mem + kRingLds);
   lds_u16 *table = (lds_u16 *)table_mem;
   const int lane = threadIdx.x;
-  const uint64_t items = uint64_t(n) * kEncMaxItems;
+  // block slots per frame per pass: 64, or the largest block count of any frame when the
+  // caller had it found (FuseCrc::max_nb)
+  uint32_t slots = uint32_t(kEncMaxItems);
+  if (fuse.max_nb) {
+    const uint32_t m = uni(*fuse.max_nb);
+    slots = m < 1u ? 1u : (m < slots ? m : slots);
+  }
+  const uint64_t items = uint64_t(n) * slots;
   for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
     // slot-major items: all frames' block 0, then all block 1, ...  The blocks that exist
     // come first and are dense in blockIdx, so they spread over every XCD, shader engine
@@ -861,7 +894,7 @@ __global__ __launch_bounds__(64) void lz4_compress_blocks_kernel(
     const uint32_t f = uint32_t(it % n), kk = uint32_t(it / n);
     const uint32_t len = uni(in_lens[f]);
     const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
-    for (uint32_t k = kk; k < nb; k += kEncMaxItems) {
+    for (uint32_t k = kk; k < nb; k += slots) {
       const uint32_t bn = (len - k * kLz4Block) < kLz4Block ? (len - k * kLz4Block) : kLz4Block;
       const uintptr_t src = reinterpret_cast<uintptr_t>(in) + in_offs[f] + uint64_t(k) * kLz4Block;
       const uintptr_t slot = reinterpret_cast<uintptr_t>(out) + out_offs[f] + 7u + uint64_t(k) * kSlot;
@@ -1055,6 +1088,7 @@ int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
   if (!n) return 0;
   FuseCrc fz = fuse ? *fuse : FuseCrc();
   fz.single_done = fz.block_crc != nullptr;
+  if (fz.max_nb) lz4f_max_blocks_launch(d_in_lens, n, fz.max_nb, s);
   uint64_t items = uint64_t(n) * kEncMaxItems;
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
   // RDK_HIP_LZ4_EXACT_SEQ=1 keeps the sequence-at-a-time engine for acceleration 1 too

@@ -545,7 +545,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   __shared__ FastLds lds;
   uint16_t *table_mem = lds.table;
   const int lane = threadIdx.x;
-  const uint64_t items = uint64_t(n) * kFastMaxItems;
+  // block slots per frame per pass: 64, or the largest block count of any frame when the
+  // caller had it found (FuseCrc::max_nb)
+  uint32_t slots = uint32_t(kFastMaxItems);
+  if (fuse.max_nb) {
+    const uint32_t m = uni(*fuse.max_nb);
+    slots = m < 1u ? 1u : (m < slots ? m : slots);
+  }
+  const uint64_t items = uint64_t(n) * slots;
   for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
     // slot-major items: all frames' block 0, then all block 1, ...  The blocks that exist
     // come first and are dense in blockIdx, so they spread over every XCD, shader engine
@@ -554,7 +561,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const uint32_t f = uint32_t(it % n), kk = uint32_t(it / n);
     const uint32_t len = uni(in_lens[f]);
     const uint32_t nb = (len + kLz4Block - 1) / kLz4Block;
-    for (uint32_t k = kk; k < nb; k += kFastMaxItems) {
+    for (uint32_t k = kk; k < nb; k += slots) {
       const uint32_t bn = (len - k * kLz4Block) < kLz4Block ? (len - k * kLz4Block) : kLz4Block;
       const uintptr_t src = reinterpret_cast<uintptr_t>(in) + in_offs[f] + uint64_t(k) * kLz4Block;
       const uintptr_t slot = reinterpret_cast<uintptr_t>(out) + out_offs[f] + 7u + uint64_t(k) * kFastSlot;
@@ -615,6 +622,7 @@ int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
   FuseCrc fz = fuse ? *fuse : FuseCrc();
   fz.single_done = fz.block_crc != nullptr;
+  if (fz.max_nb) lz4f_max_blocks_launch(d_in_lens, n, fz.max_nb, s);
   hipLaunchKernelGGL(lz4_fast_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
                      d_in_lens, d_out, d_out_offs, d_out_lens, n, fz);
   lz4f_assemble_launch(d_in, d_in_offs, d_in_lens, d_out, d_out_offs, d_out_lens, n, s,

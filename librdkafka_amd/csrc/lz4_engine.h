@@ -34,6 +34,15 @@ struct FuseCrc {
   // Set by an engine whose block kernel finishes the batches of single-block frames itself
   // (lz4_finish_wave.h); the assembler then passes over them.
   bool single_done = false;
+  // One spare device word (optional): with thousands of frames the block kernels first find
+  // the largest block count of any frame there, so that their slot-major item loop does not
+  // visit 64 block slots of frames that have one.
+  uint32_t *max_nb = nullptr;
 };
+
+// Largest block count of any of the n frames -> *d_max_nb (one small launch).
+void lz4f_max_blocks_launch(const uint32_t *d_in_lens, uint32_t n, uint32_t *d_max_nb, void *stream);
+// Above this many frames the launch above pays (fewer: the empty slots are a few loop turns).
+constexpr uint32_t kMaxNbFrames = 4096;
 
 }  // namespace rdk

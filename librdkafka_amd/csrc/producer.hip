@@ -232,8 +232,9 @@ RDK_API int rdk_hip_msgset_v2_finalize(const void *d_in, const uint64_t *d_rec_o
   // codec choice, finishes the header and combines the batch's CRC from those registers.
   // Frame i goes 61 bytes into batch i's output slot: same offsets on a shifted base.
   FuseCrc fz;
-  fz.block_crc = crc_scratch(c, s, size_t(n) * 64 * sizeof(uint32_t));
+  fz.block_crc = crc_scratch(c, s, (size_t(n) * 64 + 16) * sizeof(uint32_t));
   if (!fz.block_crc) return RDK_HIP_E_NOMEM;
+  if (n > kMaxNbFrames) fz.max_nb = fz.block_crc + size_t(n) * 64;
   fz.t0 = crc_tables_dev(c->device);
   fz.x2n = crc_x2n_dev(c->device);
   fz.batch_lens = d_batch_lens;

@@ -7,11 +7,11 @@ run() {
   case "$1" in
     finalize_fast) $P writer_finalize_fast_1MiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload finalize_fast --steps 10 ;;
     finalize) $P writer_finalize_1MiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload finalize --steps 10 ;;
-    finalize_fast_16k) $P writer_finalize_fast_16KiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload finalize_fast --batch-bytes 16384 --partitions 32768 --steps 10 ;;
-    finalize_fast_64k) $P writer_finalize_fast_64KiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload finalize_fast --batch-bytes 65536 --partitions 8192 --steps 10 ;;
+    finalize_fast_16k) $P writer_finalize_fast_16KiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel,lz4f_max_blocks_kernel" --workload finalize_fast --batch-bytes 16384 --partitions 32768 --steps 10 ;;
+    finalize_fast_64k) $P writer_finalize_fast_64KiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel,lz4f_max_blocks_kernel" --workload finalize_fast --batch-bytes 65536 --partitions 8192 --steps 10 ;;
     finalize_fast_256k) $P writer_finalize_fast_256KiB_json "lz4_fast_blocks_kernel,lz4f_assemble_kernel" --workload finalize_fast --batch-bytes 262144 --partitions 2048 --steps 10 ;;
-    finalize_16k) $P writer_finalize_16KiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload finalize --batch-bytes 16384 --partitions 32768 --steps 10 ;;
-    finalize_64k) $P writer_finalize_64KiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload finalize --batch-bytes 65536 --partitions 8192 --steps 10 ;;
+    finalize_16k) $P writer_finalize_16KiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel,lz4f_max_blocks_kernel" --workload finalize --batch-bytes 16384 --partitions 32768 --steps 10 ;;
+    finalize_64k) $P writer_finalize_64KiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel,lz4f_max_blocks_kernel" --workload finalize --batch-bytes 65536 --partitions 8192 --steps 10 ;;
     finalize_256k) $P writer_finalize_256KiB_json "lz4_compress_blocks_kernel,lz4f_assemble_kernel" --workload finalize --batch-bytes 262144 --partitions 2048 --steps 10 ;;
     consumer_16k) $P consumer_crc_verify_lz4f_decompress_16KiB "crc32c_msgset_v2,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_seq_kernel,lz4f_finish_kernel" --workload consumer --batch-bytes 16384 --partitions 32768 --steps 10 ;;
     consumer_64k) $P consumer_crc_verify_lz4f_decompress_64KiB "crc32c_msgset_v2,lz4f_walk_kernel,lz4f_blocks_kernel,lz4f_seq_kernel,lz4f_finish_kernel" --workload consumer --batch-bytes 65536 --partitions 8192 --steps 10 ;;

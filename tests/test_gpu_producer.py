@@ -139,12 +139,15 @@ def test_msgset_v2_finalize_device_batches(engine, oracle_mod, mode):
         _check_batch(oracle_mod, hdr, rec, out, int(cr[i]), "snappy" if mode == 2 else mode == 0)
 
 
+@pytest.mark.parametrize("count", [2200, 4300])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_msgset_v2_finalize_thousands_of_multiblock_batches(engine, oracle_mod, mode):
+def test_msgset_v2_finalize_thousands_of_multiblock_batches(engine, oracle_mod, mode, count):
     """more than 2048 MessageSets of several blocks each in one call: the finalizing frame
     assembler then runs in small workgroups (header, slide, codec choice, CRC terms per block);
-    8 distinct MessageSets rotated, every finished batch compared with the first of its kind
-    and those checked field by field against the oracle, all batches CRC-verified"""
+    more than 4096: the block kernels visit as many block slots per frame as the longest frame
+    has blocks (found by a launch of its own).  8 distinct MessageSets rotated, every finished
+    batch compared with the first of its kind and those checked field by field against the
+    oracle, all batches CRC-verified"""
     import numpy as np
     import torch
     rnd = random.Random(90 + mode)
@@ -154,7 +157,7 @@ def test_msgset_v2_finalize_thousands_of_multiblock_batches(engine, oracle_mod, 
         rec = W.gen_json(n, 300 + j) if j != 3 else rnd.randbytes(n)   # j == 3: kept plain
         kinds.append((W.v2_header(j, 61 + n), rec))
     slot = 200704
-    n = 2200
+    n = count
     host = np.zeros(len(kinds) * slot, dtype=np.uint8)
     for j, (hdr, rec) in enumerate(kinds):
         host[j * slot:j * slot + 61] = np.frombuffer(hdr, dtype=np.uint8)

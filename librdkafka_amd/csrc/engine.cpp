@@ -343,5 +343,5 @@ RDK_API void rdk_hip_ctx_counts(uint64_t out[2]) {
 RDK_API const char *rdk_hip_last_error(void) { return rdk::last_error(); }
 
 RDK_API const char *rdk_hip_version(void) {
-  return "librdkafka_hip 0.5 gfx950 crc32c:group16-bytetab-lds lz4c:window64-exact+round64-fast+fused-crc+seq-queue+units-lds lz4hc:3-12-lds-build lz4d:seg64-parallel snappy:window64-exact+fragment-decode dropin:combined-callers";
+  return "librdkafka_hip 0.6 gfx950 crc32c:group16-bytetab-lds lz4c:window64-exact+round64-fast+wave-finish+seq-queue+units-lds lz4hc:3-12-lds-build lz4d:seg64-parallel snappy:window64-exact+fragment-decode dropin:combined-callers";
 }

@@ -1088,6 +1088,8 @@ int lz4f_compress_device(Ctx *c, const uint8_t *d_in, const uint64_t *d_in_offs,
   if (!n) return 0;
   FuseCrc fz = fuse ? *fuse : FuseCrc();
   fz.single_done = fz.block_crc != nullptr;
+  // (without a caller's spare word: d_out_lens is not written before the assembler runs)
+  if (!fuse && n > kMaxNbFrames) fz.max_nb = d_out_lens;
   if (fz.max_nb) lz4f_max_blocks_launch(d_in_lens, n, fz.max_nb, s);
   uint64_t items = uint64_t(n) * kEncMaxItems;
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);

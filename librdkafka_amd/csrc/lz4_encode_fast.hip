@@ -622,6 +622,8 @@ int lz4f_compress_fast_device(const uint8_t *d_in, const uint64_t *d_in_offs,
   const unsigned grid = unsigned(items < 2560u * 8u ? items : 2560u * 8u);
   FuseCrc fz = fuse ? *fuse : FuseCrc();
   fz.single_done = fz.block_crc != nullptr;
+  // (without a caller's spare word: d_out_lens is not written before the assembler runs)
+  if (!fuse && n > kMaxNbFrames) fz.max_nb = d_out_lens;
   if (fz.max_nb) lz4f_max_blocks_launch(d_in_lens, n, fz.max_nb, s);
   hipLaunchKernelGGL(lz4_fast_blocks_kernel, dim3(grid), dim3(64), 0, s, d_in, d_in_offs,
                      d_in_lens, d_out, d_out_offs, d_out_lens, n, fz);

@@ -340,13 +340,15 @@ def test_batch_scale_roundtrip_property(engine):
     assert all(size / 3.2 < int(ol[i]) < size / 2.2 for i in range(4)), ol[:4]
 
 
-def test_thousands_of_multiblock_frames(engine, oracle_mod):
+@pytest.mark.parametrize("n", [2300, 4400])
+def test_thousands_of_multiblock_frames(engine, oracle_mod, n):
     """more than 2048 frames of several blocks each (the frame assembler then runs in small
-    workgroups and still has to slide every block down to its place, raw blocks included):
-    a sample of frames byte-identical to the reference's, every frame decoded back"""
+    workgroups and still has to slide every block down to its place, raw blocks included;
+    more than 4096: the block kernel visits as many block slots per frame as the longest
+    frame has blocks): a sample of frames byte-identical to the reference's, every frame
+    decoded back"""
     import numpy as np
     import torch
-    n = 2300
     sizes = [150000, 65536, 65537, 200001, 131072, 70000, 13, 0]
     pieces = [engine.gen_json(sz, 900 + j) if j != 3 else bytes(random.Random(5).randbytes(sz))
               for j, sz in enumerate(sizes)]  # (j == 3: incompressible, its blocks are stored raw)

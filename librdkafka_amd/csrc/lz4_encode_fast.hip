@@ -97,6 +97,7 @@ struct BlockCtx {
   int cold;            // rounds in a row without a single verified match (dense rounds)
   bool sparse;         // the rounds in progress are the sparse ones
   bool trig;           // this run of rounds was told to end (rend pulled in): the mode changes
+  int back;            // where the dense rounds resume after the sparse ones
 };
 
 // Per round the lane's own 36-byte window (Win, loaded three rounds ahead),
@@ -315,6 +316,21 @@ __device__ __forceinline__ void round_walk(BlockCtx &b, const Win &x, const Cand
   const int p0 = __builtin_amdgcn_readfirstlane(b.p);
   const uint64_t vm = m.vm;
   int len = m.len;
+  if constexpr (S == kSparse) {
+    // A sparse round takes no match: the first one it sees ends the sparse rounds, and the
+    // dense rounds resume at the start of the round BEFORE this one -- a match seen here has
+    // its candidate from an earlier round at the latest, so the data may have begun to match
+    // anywhere in the round before -- and parse from there position by position.  (The
+    // positions the sparse rounds have entered find themselves in the table then and go
+    // without a candidate: one in eight.)
+    const int f0 = ((p0 - R > 0 ? p0 - R : 0) + S - 1) / S;
+    if (f0 < 64 && (vm >> f0)) {
+      b.rend = min(b.rend, R + 64 * S);
+      b.back = max(R - 64 * S, b.back);  // (b.back: where these sparse rounds began)
+      b.trig = true;
+    }
+    return;
+  }
 
   // Greedy walk: first verified position at or after the end of the last match.  Every lane
   // works out its own successor (the first verified lane at or past the end of its match), so
@@ -358,9 +374,7 @@ __device__ __forceinline__ void round_walk(BlockCtx &b, const Win &x, const Cand
   // end of the NEXT round, whose positions the lookup ahead has already entered: the loop
   // then drains by itself.  (Only the position-by-position rounds count: a block that has
   // earned the stride of two matches well, and its rounds keep their loop bound in a
-  // register.)  The first match a sparse round finds ends the sparse rounds at once: only
-  // that match is taken, and the dense rounds resume right behind it (fast_block).
-  if constexpr (S == kSparse) chosen &= 0ull - chosen;
+  // register.)
   if (!chosen) {
     if constexpr (S == 1 && RDK_FAST_SPARSE) {
       if (!vm && xin < 64 * S && ++b.cold == kColdRounds) {
@@ -370,12 +384,7 @@ __device__ __forceinline__ void round_walk(BlockCtx &b, const Win &x, const Cand
     }
     return;
   }
-  if constexpr (S == kSparse) {
-    b.rend = min(b.rend, R + 64 * S);
-    b.trig = true;
-  } else if constexpr (S == 1) {
-    b.cold = 0;
-  }
+  if constexpr (S == 1) b.cold = 0;
   const int lastq = 63 - int(__builtin_clzll(chosen));
   b.p = R + S * lastq + __builtin_amdgcn_readlane(len, lastq);
 
@@ -494,6 +503,7 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, FastLds *lds, int
   b.full = false;
 
   b.sparse = b.trig = false;
+  b.back = 0;
   int S = 1;                        // stride of the dense rounds
   bool decided = !RDK_FAST_STRIDE2;  // ... once the block's first kProbe positions have decided it
   for (int r0 = 0;;) {
@@ -506,6 +516,7 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, FastLds *lds, int
     }
     b.rend = (!decided && !b.sparse) ? kProbe : n;
     b.cold = 0;
+    b.back = r0;
     if (b.sparse) fast_rounds<kSparse>(b, lds, r0, lane);
     else if (S == 2) fast_rounds<2>(b, lds, r0, lane);
     else fast_rounds<1>(b, lds, r0, lane);
@@ -513,10 +524,8 @@ __device__ int fast_block(uintptr_t src, int n, uintptr_t dst, FastLds *lds, int
     if (__builtin_amdgcn_readfirstlane(int(b.full)) || rend >= n || b.mfl < rend) break;
     r0 = rend;
     if (__builtin_amdgcn_readfirstlane(int(b.trig))) {
-      // (out of the sparse rounds: on from the end of the match that ended them; the few
-      // positions the last lookup ahead entered for a round that was not parsed find
-      // themselves in the table and go without a candidate)
-      if (b.sparse) r0 = __builtin_amdgcn_readfirstlane(b.p);
+      // (out of the sparse rounds: back to the start of the round that saw a match)
+      if (b.sparse) r0 = __builtin_amdgcn_readfirstlane(b.back);
       b.sparse = !b.sparse;
     }
     b.trig = false;

@@ -467,7 +467,8 @@ def test_fast_compress_ratio_within_5pct(engine, oracle_mod, units):
 
 def test_fast_compress_data_that_stops_and_starts_matching(engine, oracle_mod):
     """Stretches without matches (random bytes) put the wave engine's rounds at every eighth
-    position, the first match brings them back: blocks that change between the two, at
+    position, the first match seen brings the dense rounds back (from a round earlier):
+    blocks that change between the two, at
     several stretch lengths and in both orders, decode to their input, and the ratio stays
     within 5 % of the reference's (whose own search step grows over such stretches)."""
     rnd = random.Random(46)
